@@ -1,0 +1,202 @@
+/*
+ * lsp.h -- C-ABI of liblsp_hip.so, the MI355X-native hot path of
+ * distributed-lab/linea-stark-prover.
+ *
+ * The reference plugs its prover together from Plonky3 type aliases
+ * (bin/src/config.rs:9-25) and calls p3_uni_stark::prove/verify
+ * (bin/src/main.rs:80-96).  Every entry point below replaces one trait method
+ * or free function reachable from that plug point; the comment on each cites
+ * the reference call site (file:line in the reference repo) and the Plonky3
+ * item ([EXT] = distributed-lab/Plonky3@f888f90, Cargo.lock:505-711, not
+ * vendored) it stands in for.  INTEGRATION.md shows the Rust-side binding.
+ *
+ * Conventions
+ *   - Elements: lsp_fr = 4 x u64 little-endian limbs in Montgomery form with
+ *     R = 2^256, canonical in [0, r) -- ark-ff 0.5's in-memory Fr, so a
+ *     &[Bls12_377Fr] can be passed as *const lsp_fr once the shim asserts
+ *     size_of::<Bls12_377Fr>() == 32.
+ *   - Matrices: row-major, height x width (p3-matrix RowMajorMatrix).
+ *   - `mem`: LSP_MEM_HOST = pointers are host memory (copied in/out),
+ *     LSP_MEM_DEVICE = pointers are device memory on the context's GPU
+ *     (allocated with lsp_dev_alloc or any HIP allocation on that device).
+ *   - Errors: every call returns LSP_OK (0) or an LSP_E_* code; the message is
+ *     in lsp_last_error(ctx).  Plonky3 panics where these return non-zero, so
+ *     the Rust shim panics on non-zero status (except verify).
+ *   - Threading: a context is bound to one device and one HIP stream and is
+ *     serialised by an internal mutex; calls are synchronous at return.
+ */
+#ifndef LSP_H
+#define LSP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct { uint64_t l[4]; } lsp_fr;
+
+enum {
+    LSP_OK = 0,
+    LSP_E_ARG = 1,     /* bad argument (null pointer, bad descriptor, ...) */
+    LSP_E_OOM = 2,     /* device or host allocation failed */
+    LSP_E_HIP = 3,     /* HIP runtime error */
+    LSP_E_SIZE = 4,    /* height not a power of two / too large */
+    LSP_E_VERIFY = 5,  /* proof rejected */
+    LSP_E_STATE = 6    /* no GPU / context unusable */
+};
+
+enum { LSP_MEM_HOST = 0, LSP_MEM_DEVICE = 1 };
+
+/* AIR descriptor (int32 array) -- the AirConfig list of LineaAIR
+ * (air/src/lib.rs:11-54), i.e. what LineaAIR::eval iterates:
+ *   [n_configs, config_0, config_1, ...]
+ * LSP_AIR_PERMUTATION (AirPermutationConfig, air/src/air_permutation.rs:1-24):
+ *   1, na, nb, a_ids[na], b_ids[nb], b_inverse_id, check_id
+ * LSP_AIR_LOOKUP (AirLookupConfig, air/src/air_lookup.rs:1-40):
+ *   2, na, a_ids[na], ntables, ncols, b_ids[ntables*ncols], a_filter_id,
+ *   b_filter_ids[ntables], a_inverses_id, b_inverses_ids[ntables],
+ *   occurrences_ids[ntables], check_id
+ * Column ids are absolute (already shifted, trace/src/lib.rs:40-58). */
+enum { LSP_AIR_PERMUTATION = 1, LSP_AIR_LOOKUP = 2 };
+
+typedef struct lsp_ctx lsp_ctx;
+typedef struct lsp_tree lsp_tree;
+typedef struct lsp_proof lsp_proof;
+
+/* StarkConfig / FriConfig / Perm parameters (bin/src/config.rs:9-25,
+ * bin/src/main.rs:49-64). */
+typedef struct {
+    uint32_t sbox_degree;          /* U1: 11 (default) or 17 */
+    uint32_t rounds_f;             /* full rounds, 8 (bin/src/main.rs:49) */
+    uint32_t rounds_p;             /* partial rounds, 22 (bin/src/main.rs:49) */
+    const lsp_fr *round_constants; /* 3*rounds_f + rounds_p, new_from_rng order:
+                                      initial external, terminal external, internal */
+    uint32_t log_blowup;           /* 3  (bin/src/main.rs:59) */
+    uint32_t log_final_poly_len;   /* 0  (bin/src/main.rs:60) */
+    uint32_t num_queries;          /* 33 (bin/src/main.rs:61) */
+    uint32_t proof_of_work_bits;   /* 0  (bin/src/main.rs:62) */
+    int32_t public_degree;         /* U6: symbolic degree of a public value, 1 (fork, default) or 0 */
+} lsp_params;
+
+/* ---------------------------------------------------------------- library */
+const char *lsp_version(void);
+int lsp_device_count(int *n);
+const char *lsp_last_error(const lsp_ctx *ctx);
+
+/* U4/U5: documented seeded generator replacing thread_rng() for the
+ * challenges (bin/src/main.rs:29-31) and Perm::new_from_rng (bin/src/main.rs:49).
+ * round_constants must hold 3*rounds_f + rounds_p elements. */
+int lsp_seeded_setup(uint64_t seed, uint32_t rounds_f, uint32_t rounds_p, lsp_fr *alpha, lsp_fr *delta,
+                     lsp_fr *round_constants);
+
+/* Field conversions (host).  from_be_bytes_mod_order replaces
+ * FF_Bls12_377Fr::from_be_bytes_mod_order (trace/src/permutation.rs:102-104). */
+void lsp_fr_from_canonical(const uint64_t in[4], lsp_fr *out);
+void lsp_fr_to_canonical(const lsp_fr *in, uint64_t out[4]);
+void lsp_fr_from_be_bytes_mod_order(const uint8_t *be, size_t n, lsp_fr *out);
+void lsp_fr_mul(const lsp_fr *a, const lsp_fr *b, lsp_fr *out);
+void lsp_fr_inv(const lsp_fr *a, lsp_fr *out);
+void lsp_two_adic_generator(uint32_t bits, lsp_fr *out); /* TwoAdicField::two_adic_generator */
+
+/* ---------------------------------------------------------------- context */
+/* device = LSP_HOST_ONLY creates a verifier-only context that never touches
+ * a GPU (lsp_verify, lsp_merkle_verify work; device entry points return
+ * LSP_E_STATE). */
+#define LSP_HOST_ONLY (-1)
+int lsp_ctx_create(int device, const lsp_params *params, lsp_ctx **out);
+int lsp_ctx_destroy(lsp_ctx *ctx);
+int lsp_synchronize(lsp_ctx *ctx);
+int lsp_dev_alloc(lsp_ctx *ctx, size_t bytes, void **dptr);
+int lsp_dev_free(lsp_ctx *ctx, void *dptr);
+int lsp_memcpy_h2d(lsp_ctx *ctx, void *dst, const void *src, size_t bytes);
+int lsp_memcpy_d2h(lsp_ctx *ctx, void *dst, const void *src, size_t bytes);
+
+/* ------------------------------------------------------------------- Dft */
+/* TwoAdicSubgroupDft::coset_lde_batch(mat, added_bits, shift) followed by
+ * .bit_reverse_rows().to_row_major_matrix(), as TwoAdicFriPcs::commit uses it
+ * ([EXT p3-dft Radix2DitParallel], bin/src/config.rs:22; bin/src/main.rs:52).
+ * in: h x w values on H_h; out: (h << added_bits) x w, row i = p(shift * w_N^bitrev(i)). */
+int lsp_coset_lde_batch(lsp_ctx *ctx, const lsp_fr *in, size_t h, size_t w, uint32_t added_bits,
+                        const lsp_fr *shift, lsp_fr *out, int mem);
+/* Same with one shift per column (the quotient-chunk commit of p3-uni-stark,
+ * where chunk j uses GEN / (GEN * w_Q^j)). */
+int lsp_coset_lde_batch_shifts(lsp_ctx *ctx, const lsp_fr *in, size_t h, size_t w, uint32_t added_bits,
+                               const lsp_fr *shifts, lsp_fr *out, int mem);
+
+/* ---------------------------------------------------- Poseidon2 / symmetric */
+/* Poseidon2Bls12337<3>::permute_mut on n states of 3 (bin/src/config.rs:11) */
+int lsp_poseidon2_permute_batch(lsp_ctx *ctx, lsp_fr *states, size_t n, int mem);
+/* PaddingFreeSponge<Perm,3,2,1>::hash_iter of each of n rows of width w
+ * (bin/src/config.rs:12) */
+int lsp_hash_rows(lsp_ctx *ctx, const lsp_fr *rows, size_t n, size_t w, lsp_fr *out, int mem);
+
+/* ------------------------------------------------------------------ Mmcs */
+/* MerkleTreeMmcs::commit over nmats equal-height row-major matrices
+ * (bin/src/config.rs:19-20): leaf = hash_iter of the rows concatenated in
+ * commit order (U11); nodes = CompressionFunctionFromHasher (bin/src/config.rs:17). */
+int lsp_merkle_commit(lsp_ctx *ctx, const lsp_fr *const *mats, const size_t *widths, size_t nmats,
+                      size_t height, int mem, lsp_fr *root, lsp_tree **tree);
+/* Mmcs::open_batch: rows_out gets sum(widths) elements, path_out log2(height) digests */
+int lsp_merkle_open(const lsp_tree *tree, size_t index, lsp_fr *rows_out, lsp_fr *path_out);
+/* digest layer `level` (0 = leaf digests) -> out (height >> level elements) */
+int lsp_merkle_layer(const lsp_tree *tree, uint32_t level, lsp_fr *out);
+/* Mmcs::verify_batch (host) -- LSP_OK or LSP_E_VERIFY */
+int lsp_merkle_verify(const lsp_ctx *ctx, const lsp_fr *root, const size_t *widths, size_t nmats,
+                      uint32_t log_height, size_t index, const lsp_fr *rows, const lsp_fr *path);
+int lsp_tree_free(lsp_tree *tree);
+
+/* ----------------------------------------------------------- FriFolder */
+/* TwoAdicFriGenericConfig::fold_matrix(beta, RowMajorMatrix(v, 2)) [EXT p3-fri]:
+ * out[i] = (1/2 + beta/2 g^-bitrev(i)) v[2i] + (1/2 - beta/2 g^-bitrev(i)) v[2i+1],
+ * g = w_len.  len = length of v (power of two >= 2); out has len/2. */
+int lsp_fri_fold(lsp_ctx *ctx, const lsp_fr *v, size_t len, const lsp_fr *beta, lsp_fr *out, int mem);
+/* TwoAdicFriGenericConfig::fold_row (host; verifier side) */
+void lsp_fri_fold_row(size_t index, uint32_t log_height, const lsp_fr *beta, const lsp_fr *e0,
+                      const lsp_fr *e1, lsp_fr *out);
+
+/* ------------------------------------------------------------- quotient */
+/* log_quotient_degree from the symbolic constraint degrees (U6 rule) */
+int lsp_log_quotient_degree(const int32_t *air, size_t air_len, int32_t public_degree, uint32_t *log_q);
+/* p3-uni-stark quotient_values over the LDE of the trace (row-major,
+ * bit-reversed, (h << log_blowup) x w) with LineaAIR::eval
+ * (air/src/lib.rs:47-167): out[i], i < h << log_q, natural order on GEN*H_Q. */
+int lsp_quotient_values(lsp_ctx *ctx, const lsp_fr *lde, size_t h, size_t w, const int32_t *air, size_t air_len,
+                        const lsp_fr *public_values, size_t npub, const lsp_fr *alpha, lsp_fr *out, int mem);
+
+/* ------------------------------------------------------------- PCS open */
+/* interpolate_coset [EXT p3-interpolation] of the first h rows of a bit-reversed
+ * LDE (the low coset shift*H_h) at z: ys_out gets w values (host memory). */
+int lsp_interpolate_coset(lsp_ctx *ctx, const lsp_fr *lde_bitrev, size_t h, size_t w, const lsp_fr *shift,
+                          const lsp_fr *z, lsp_fr *ys_out, int mem);
+/* p3-field batch_multiplicative_inverse */
+int lsp_batch_inverse(lsp_ctx *ctx, const lsp_fr *in, size_t n, lsp_fr *out, int mem);
+
+/* ----------------------------------------------------------------- prove */
+/* p3_uni_stark::prove(config, air, challenger, trace, public_values)
+ * (bin/src/main.rs:80-86) with Challenger = HashChallenger::new(vec![], hash)
+ * (bin/src/main.rs:78).  trace: h x w row-major. */
+int lsp_prove(lsp_ctx *ctx, const lsp_fr *trace, size_t h, size_t w, const int32_t *air, size_t air_len,
+              const lsp_fr *public_values, size_t npub, int mem, lsp_proof **out);
+/* serialized proof (format in DESIGN.md); buf == NULL -> *len = required size */
+int lsp_proof_serialize(const lsp_proof *proof, uint8_t *buf, size_t cap, size_t *len);
+int lsp_proof_free(lsp_proof *proof);
+/* p3_uni_stark::verify (bin/src/main.rs:88-96) on the host CPU */
+int lsp_verify(const lsp_ctx *ctx, const int32_t *air, size_t air_len, const lsp_fr *public_values, size_t npub,
+               const uint8_t *proof, size_t len);
+/* per-phase device times of the last lsp_prove (ms), span names as in the
+ * reference's bench.log */
+int lsp_last_timings(const lsp_ctx *ctx, double *ms, const char **names, size_t cap, size_t *n);
+
+/* ------------------------------------------------------------- witness */
+/* Synthetic permutation trace with the witness columns of
+ * RawPermutationTrace::get_trace (trace/src/permutation.rs:24-93):
+ * row-major h x (2*ncols + 2), h = 2^log_n. */
+int lsp_gen_permutation_trace(uint64_t seed, uint32_t log_n, uint32_t ncols, const lsp_fr *alpha,
+                              const lsp_fr *delta, int small_values, lsp_fr *rows_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LSP_H */

@@ -1,0 +1,92 @@
+"""Build liblsp_hip.so (HIP kernels + host orchestration) for gfx950, in-tree.
+
+    python -m linea_stark_prover_amd.build [--force] [-j N]
+
+Objects go to ``linea_stark_prover_amd/_build/``, the library to
+``linea_stark_prover_amd/_lib/liblsp_hip.so`` (git-ignored, travels to the GPU
+box with the snapshot).  Rebuilds only what changed (any header change
+rebuilds everything).
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(PKG, "_build")
+LIBDIR = os.path.join(PKG, "_lib")
+LIB = os.path.join(LIBDIR, "liblsp_hip.so")
+ARCH = os.environ.get("LSP_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+SOURCES = ["k_ntt.hip", "k_hash.hip", "k_field.hip", "k_quotient.hip", "k_open.hip",
+           "host.cpp", "prove.cpp", "verify.cpp", "capi.cpp"]
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
+          "-Wno-unused-variable", "-I", os.path.join(ROOT, "include")]
+
+
+def _headers():
+    return [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hpp")] + \
+        [os.path.join(ROOT, "include", "lsp.h")]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src):
+    obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+    cmd = [HIPCC] + CFLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
+    if src.endswith(".cpp"):
+        cmd = [HIPCC] + CFLAGS + ["-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(force: bool = False, jobs: int = None, verbose: bool = True) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
+    hdrs = _headers()
+    todo = []
+    objs = []
+    for s in SOURCES:
+        obj = os.path.join(BUILD, os.path.splitext(s)[0] + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [os.path.join(CSRC, s)] + hdrs):
+            todo.append(s)
+    jobs = jobs or min(len(todo) or 1, os.cpu_count() or 4, 16)
+    if todo:
+        if verbose:
+            print(f"[lsp build] compiling {len(todo)} file(s) for {ARCH}: {' '.join(todo)}", flush=True)
+        with cf.ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(_compile, todo))
+    if todo or _stale(LIB, objs):
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs + ["-lpthread"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        if verbose:
+            print(f"[lsp build] linked {LIB}", flush=True)
+    return LIB
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", type=int, default=None)
+    a = ap.parse_args(argv)
+    build(a.force, a.j)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

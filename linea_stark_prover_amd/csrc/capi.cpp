@@ -1,0 +1,630 @@
+// extern "C" entry points of liblsp_hip.so (declared in include/lsp.h).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+
+#include "prove_internal.hpp"
+
+using namespace lsp;
+
+namespace {
+thread_local std::string g_err;  // errors without a context
+
+template <class F>
+int guarded(lsp_ctx* ctx, F&& f) {
+    try {
+        f();
+        return LSP_OK;
+    } catch (const LspError& e) {
+        (ctx ? ctx->err : g_err) = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        (ctx ? ctx->err : g_err) = "host allocation failed";
+        return LSP_E_OOM;
+    } catch (const std::exception& e) {
+        (ctx ? ctx->err : g_err) = e.what();
+        return LSP_E_STATE;
+    }
+}
+
+// device input: either the caller's device pointer or a pool copy of host data
+const Fr* dev_in(lsp_ctx* ctx, const lsp_fr* p, size_t n, int mem, const char* name) {
+    LSP_REQUIRE(p || n == 0, LSP_E_ARG, "null input pointer");
+    if (mem == LSP_MEM_DEVICE) return reinterpret_cast<const Fr*>(p);
+    LSP_REQUIRE(mem == LSP_MEM_HOST, LSP_E_ARG, "mem must be LSP_MEM_HOST or LSP_MEM_DEVICE");
+    Fr* d = ctx->fbuf(name, n ? n : 1);
+    if (n) LSP_HIP(hipMemcpyAsync(d, p, n * sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+    return d;
+}
+Fr* dev_out(lsp_ctx* ctx, lsp_fr* p, size_t n, int mem, const char* name) {
+    LSP_REQUIRE(p || n == 0, LSP_E_ARG, "null output pointer");
+    if (mem == LSP_MEM_DEVICE) return reinterpret_cast<Fr*>(p);
+    return ctx->fbuf(name, n ? n : 1);
+}
+void finish_out(lsp_ctx* ctx, lsp_fr* p, const Fr* d, size_t n, int mem) {
+    if (mem == LSP_MEM_HOST && n)
+        LSP_HIP(hipMemcpyAsync(p, d, n * sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+}
+
+void need_gpu(lsp_ctx* ctx) {
+    LSP_REQUIRE(ctx, LSP_E_ARG, "null ctx");
+    LSP_REQUIRE(ctx->device != LSP_HOST_ONLY, LSP_E_STATE, "host-only context (LSP_HOST_ONLY) has no GPU");
+    LSP_HIP(hipSetDevice(ctx->device));
+}
+
+struct SplitMix64 {
+    uint64_t s;
+    uint64_t next() {
+        uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
+    }
+    // U4: 4 words -> 253-bit mask -> reject >= r
+    Fr fr() {
+        for (;;) {
+            Fr c;
+            for (int k = 0; k < 4; ++k) {
+                uint64_t x = next();
+                c.v[2 * k] = (uint32_t)x;
+                c.v[2 * k + 1] = (uint32_t)(x >> 32);
+            }
+            c.v[7] &= (1u << 29) - 1;
+            if (fr_words_lt_mod(c)) return fr_from_canonical(c);
+        }
+    }
+    uint64_t below(uint64_t n) {
+        const unsigned __int128 two64 = (unsigned __int128)1 << 64;
+        const unsigned __int128 lim = two64 - (two64 % n);
+        for (;;) {
+            uint64_t x = next();
+            if ((unsigned __int128)x < lim) return x % n;
+        }
+    }
+};
+}  // namespace
+
+extern "C" {
+
+const char* lsp_version(void) { return "linea_stark_prover_amd 0.1 (gfx950)"; }
+
+int lsp_device_count(int* n) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(n, LSP_E_ARG, "null");
+        int c = 0;
+        if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+        *n = c;
+    });
+}
+
+const char* lsp_last_error(const lsp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int lsp_seeded_setup(uint64_t seed, uint32_t rounds_f, uint32_t rounds_p, lsp_fr* alpha, lsp_fr* delta,
+                     lsp_fr* rc) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(alpha && delta && rc && rounds_f % 2 == 0, LSP_E_ARG, "bad seeded_setup arguments");
+        SplitMix64 g{seed};
+        *alpha = from_fr(g.fr());
+        *delta = from_fr(g.fr());
+        for (uint32_t i = 0; i < 3 * rounds_f + rounds_p; ++i) rc[i] = from_fr(g.fr());
+    });
+}
+
+void lsp_fr_from_canonical(const uint64_t in[4], lsp_fr* out) {
+    lsp_fr t;
+    std::memcpy(t.l, in, 32);
+    *out = from_fr(fr_from_canonical(to_fr(t)));
+}
+void lsp_fr_to_canonical(const lsp_fr* in, uint64_t out[4]) {
+    lsp_fr t = from_fr(fr_to_canonical(to_fr(*in)));
+    std::memcpy(out, t.l, 32);
+}
+void lsp_fr_from_be_bytes_mod_order(const uint8_t* be, size_t n, lsp_fr* out) {
+    // Horner over bytes: acc = acc * 256 + byte (mod r)
+    const Fr b256 = fr_from_u64(256);
+    Fr acc = fr_zero();
+    for (size_t i = 0; i < n; ++i) acc = fr_add(fr_mul(acc, b256), fr_from_u64(be[i]));
+    *out = from_fr(acc);
+}
+void lsp_fr_mul(const lsp_fr* a, const lsp_fr* b, lsp_fr* out) { *out = from_fr(fr_mul(to_fr(*a), to_fr(*b))); }
+void lsp_fr_inv(const lsp_fr* a, lsp_fr* out) { *out = from_fr(fr_inv(to_fr(*a))); }
+void lsp_two_adic_generator(uint32_t bits, lsp_fr* out) {
+    if (bits > 47) bits = 47;
+    *out = from_fr(host_two_adic_generator(bits));
+}
+
+int lsp_ctx_create(int device, const lsp_params* p, lsp_ctx** out) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(p && out && p->round_constants, LSP_E_ARG, "null params");
+        LSP_REQUIRE(p->sbox_degree == 11 || p->sbox_degree == 17, LSP_E_ARG, "S-box degree must be 11 or 17");
+        LSP_REQUIRE(p->rounds_f >= 2 && p->rounds_f % 2 == 0 && p->rounds_f <= 64 && p->rounds_p <= 256, LSP_E_ARG,
+                    "bad round counts");
+        LSP_REQUIRE(p->log_blowup >= 1 && p->log_blowup <= 8 && p->num_queries >= 1 && p->num_queries <= 1024 &&
+                        p->proof_of_work_bits <= 32 && p->log_final_poly_len <= 8 &&
+                        (p->public_degree == 0 || p->public_degree == 1),
+                    LSP_E_ARG, "bad FRI parameters");
+        auto c = std::make_unique<lsp_ctx>();
+        c->device = device;
+        c->p2.L = P2Layout{p->rounds_f, p->rounds_p, p->sbox_degree};
+        const size_t nrc = 3 * p->rounds_f + p->rounds_p;
+        c->p2.rc.resize(nrc);
+        for (size_t i = 0; i < nrc; ++i) c->p2.rc[i] = to_fr(p->round_constants[i]);
+        if (device != LSP_HOST_ONLY) {  // LSP_HOST_ONLY: verifier-only context, no GPU touched
+            int n = 0;
+            if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw LspError(LSP_E_STATE, "no HIP device");
+            LSP_REQUIRE(device >= 0 && device < n, LSP_E_ARG, "bad device index");
+            LSP_HIP(hipSetDevice(device));
+            LSP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            LSP_HIP(hipMalloc(&c->rc_dev, nrc * sizeof(Fr)));
+            LSP_HIP(hipMemcpy(c->rc_dev, c->p2.rc.data(), nrc * sizeof(Fr), hipMemcpyHostToDevice));
+        }
+        c->log_blowup = p->log_blowup;
+        c->log_final_poly_len = p->log_final_poly_len;
+        c->num_queries = p->num_queries;
+        c->pow_bits = p->proof_of_work_bits;
+        c->public_degree = p->public_degree;
+        *out = c.release();
+    });
+}
+
+int lsp_ctx_destroy(lsp_ctx* ctx) {
+    if (!ctx) return LSP_OK;
+    if (ctx->device == LSP_HOST_ONLY) {
+        delete ctx;
+        return LSP_OK;
+    }
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->pool)
+        if (kv.second.p) (void)hipFree(kv.second.p);
+    for (auto& kv : ctx->twiddles) (void)hipFree(kv.second);
+    if (ctx->rc_dev) (void)hipFree(ctx->rc_dev);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return LSP_OK;
+}
+
+int lsp_synchronize(lsp_ctx* ctx) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx, LSP_E_ARG, "null ctx");
+        need_gpu(ctx);
+        LSP_HIP(hipDeviceSynchronize());
+    });
+}
+
+int lsp_dev_alloc(lsp_ctx* ctx, size_t bytes, void** dptr) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && dptr, LSP_E_ARG, "null");
+        need_gpu(ctx);
+        if (hipMalloc(dptr, bytes ? bytes : 1) != hipSuccess) {
+            (void)hipGetLastError();
+            throw LspError(LSP_E_OOM, "hipMalloc failed");
+        }
+    });
+}
+int lsp_dev_free(lsp_ctx* ctx, void* dptr) {
+    return guarded(ctx, [&] { LSP_HIP(hipFree(dptr)); });
+}
+int lsp_memcpy_h2d(lsp_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    return guarded(ctx, [&] {
+        LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+        ctx->sync();
+    });
+}
+int lsp_memcpy_d2h(lsp_ctx* ctx, void* dst, const void* src, size_t bytes) {
+    return guarded(ctx, [&] {
+        LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        ctx->sync();
+    });
+}
+
+int lsp_coset_lde_batch_shifts(lsp_ctx* ctx, const lsp_fr* in, size_t h, size_t w, uint32_t added_bits,
+                               const lsp_fr* shifts, lsp_fr* out, int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && shifts && w >= 1, LSP_E_ARG, "bad arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        log2_exact(h);
+        LSP_REQUIRE(added_bits <= 16, LSP_E_ARG, "added_bits too large");
+        const size_t N = h << added_bits;
+        std::vector<Fr> sh(w);
+        for (size_t c = 0; c < w; ++c) sh[c] = to_fr(shifts[c]);
+        const Fr* din = dev_in(ctx, in, h * w, mem, "api_in");
+        Fr* dout = dev_out(ctx, out, N * w, mem, "api_out");
+        lde_device(ctx, din, h, w, added_bits, sh.data(), dout);
+        finish_out(ctx, out, dout, N * w, mem);
+    });
+}
+
+int lsp_coset_lde_batch(lsp_ctx* ctx, const lsp_fr* in, size_t h, size_t w, uint32_t added_bits,
+                        const lsp_fr* shift, lsp_fr* out, int mem) {
+    if (!shift || w == 0) return LSP_E_ARG;
+    std::vector<lsp_fr> sh(w, *shift);
+    return lsp_coset_lde_batch_shifts(ctx, in, h, w, added_bits, sh.data(), out, mem);
+}
+
+int lsp_poseidon2_permute_batch(lsp_ctx* ctx, lsp_fr* states, size_t n, int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx, LSP_E_ARG, "null ctx");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        Fr* d = const_cast<Fr*>(dev_in(ctx, states, 3 * n, mem, "api_in"));
+        LSP_HIP(launch_permute(d, n, ctx->rc_dev, ctx->p2.L, ctx->stream));
+        finish_out(ctx, states, d, 3 * n, mem);
+    });
+}
+
+int lsp_hash_rows(lsp_ctx* ctx, const lsp_fr* rows, size_t n, size_t w, lsp_fr* out, int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx, LSP_E_ARG, "null ctx");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const Fr* din = dev_in(ctx, rows, n * w, mem, "api_in");
+        Fr* dout = dev_out(ctx, out, n, mem, "api_out");
+        MatList m{};
+        m.ptr[0] = din;
+        m.width[0] = (uint32_t)w;
+        m.n = 1;
+        LSP_HIP(launch_hash_rows(m, n, dout, ctx->rc_dev, ctx->p2.L, ctx->stream));
+        finish_out(ctx, out, dout, n, mem);
+    });
+}
+
+int lsp_merkle_commit(lsp_ctx* ctx, const lsp_fr* const* mats, const size_t* widths, size_t nmats, size_t height,
+                      int mem, lsp_fr* root, lsp_tree** tree) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && mats && widths && root && nmats >= 1 && nmats <= 8, LSP_E_ARG,
+                    "bad merkle_commit arguments (1..8 matrices)");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        log2_exact(height);
+        auto t = std::make_unique<lsp_tree>();
+        t->ctx = ctx;
+        t->height = height;
+        MatList m{};
+        m.n = (uint32_t)nmats;
+        for (size_t k = 0; k < nmats; ++k) {
+            LSP_REQUIRE(widths[k] >= 1 && mats[k], LSP_E_ARG, "bad matrix");
+            Fr* d = nullptr;
+            LSP_HIP(hipMalloc(&d, height * widths[k] * sizeof(Fr)));
+            t->mats.push_back(d);
+            t->widths.push_back(widths[k]);
+            LSP_HIP(hipMemcpyAsync(d, mats[k], height * widths[k] * sizeof(Fr),
+                                   mem == LSP_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                                   ctx->stream));
+            m.ptr[k] = d;
+            m.width[k] = (uint32_t)widths[k];
+        }
+        LSP_HIP(hipMalloc(&t->layers, (2 * height - 1) * sizeof(Fr)));
+        *root = from_fr(commit_device(ctx, m, height, t->layers));
+        if (tree)
+            *tree = t.release();
+        else {
+            for (auto* d : t->mats) (void)hipFree(d);
+            (void)hipFree(t->layers);
+        }
+    });
+}
+
+int lsp_merkle_open(const lsp_tree* t, size_t index, lsp_fr* rows_out, lsp_fr* path_out) {
+    if (!t) return LSP_E_ARG;
+    lsp_ctx* ctx = t->ctx;
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(index < t->height, LSP_E_ARG, "index out of range");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        size_t o = 0;
+        if (rows_out)
+            for (size_t k = 0; k < t->mats.size(); ++k) {
+                LSP_HIP(hipMemcpy(rows_out + o, t->mats[k] + index * t->widths[k], t->widths[k] * sizeof(Fr),
+                                  hipMemcpyDeviceToHost));
+                o += t->widths[k];
+            }
+        if (path_out) {
+            size_t off = 0, len = t->height;
+            for (uint32_t i = 0; len > 1; ++i) {
+                LSP_HIP(hipMemcpy(path_out + i, t->layers + off + ((index >> i) ^ 1), sizeof(Fr),
+                                  hipMemcpyDeviceToHost));
+                off += len;
+                len >>= 1;
+            }
+        }
+    });
+}
+
+int lsp_merkle_layer(const lsp_tree* t, uint32_t level, lsp_fr* out) {
+    if (!t || !out) return LSP_E_ARG;
+    lsp_ctx* ctx = t->ctx;
+    return guarded(ctx, [&] {
+        size_t off = 0, len = t->height;
+        for (uint32_t i = 0; i < level; ++i) {
+            LSP_REQUIRE(len > 1, LSP_E_ARG, "level out of range");
+            off += len;
+            len >>= 1;
+        }
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        LSP_HIP(hipMemcpy(out, t->layers + off, len * sizeof(Fr), hipMemcpyDeviceToHost));
+    });
+}
+
+int lsp_merkle_verify(const lsp_ctx* ctx, const lsp_fr* root, const size_t* widths, size_t nmats,
+                      uint32_t log_height, size_t index, const lsp_fr* rows, const lsp_fr* path) {
+    if (!ctx || !root || !widths || !rows || (log_height && !path)) return LSP_E_ARG;
+    size_t tot = 0;
+    for (size_t k = 0; k < nmats; ++k) tot += widths[k];
+    std::vector<Fr> leaf(tot);
+    for (size_t i = 0; i < tot; ++i) leaf[i] = to_fr(rows[i]);
+    Fr cur = ctx->p2.hash(leaf.data(), tot);
+    for (uint32_t i = 0; i < log_height; ++i) {
+        const Fr sib = to_fr(path[i]);
+        cur = ((index >> i) & 1) ? ctx->p2.compress(sib, cur) : ctx->p2.compress(cur, sib);
+    }
+    return fr_eq(cur, to_fr(*root)) ? LSP_OK : LSP_E_VERIFY;
+}
+
+int lsp_tree_free(lsp_tree* t) {
+    if (!t) return LSP_OK;
+    if (t->ctx->device != LSP_HOST_ONLY) (void)hipSetDevice(t->ctx->device);
+    for (auto* d : t->mats) (void)hipFree(d);
+    (void)hipFree(t->layers);
+    delete t;
+    return LSP_OK;
+}
+
+int lsp_fri_fold(lsp_ctx* ctx, const lsp_fr* v, size_t len, const lsp_fr* beta, lsp_fr* out, int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && beta && len >= 2, LSP_E_ARG, "bad fri_fold arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const uint32_t lg = log2_exact(len);
+        const size_t m = len / 2;
+        const Fr* din = dev_in(ctx, v, len, mem, "api_in");
+        Fr* dout = dev_out(ctx, out, m, mem, "api_out");
+        const Fr half = fr_inv(fr_from_u64(2));
+        const Fr ginv = fr_inv(host_two_adic_generator(lg));
+        uint32_t L1 = (lg - 1 + 1) / 2, L2 = (lg - 1) - L1;
+        Fr* tab = ctx->fbuf("api_tab", (1ull << L1) + (1ull << L2));
+        Fr* b = ctx->fbuf("api_tab_base", 1);
+        LSP_HIP(hipMemcpyAsync(b, &ginv, sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+        LSP_HIP(launch_pow_tables(b, 1, L1, L2, nullptr, tab, ctx->stream));
+        LSP_HIP(launch_fri_fold(din, m, half, fr_mul(to_fr(*beta), half), tab, L1, dout, ctx->stream));
+        finish_out(ctx, out, dout, m, mem);
+    });
+}
+
+void lsp_fri_fold_row(size_t index, uint32_t log_height, const lsp_fr* beta, const lsp_fr* e0, const lsp_fr* e1,
+                      lsp_fr* out) {
+    const Fr s0 = fr_pow_u64(host_two_adic_generator(log_height + 1), host_bitrev(index, log_height));
+    const Fr a = to_fr(*e0), b = to_fr(*e1);
+    const Fr r = fr_add(a, fr_mul(fr_mul(fr_sub(to_fr(*beta), s0), fr_sub(b, a)), fr_inv(fr_sub(fr_neg(s0), s0))));
+    *out = from_fr(r);
+}
+
+int lsp_log_quotient_degree(const int32_t* air, size_t air_len, int32_t public_degree, uint32_t* log_q) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(log_q, LSP_E_ARG, "null");
+        *log_q = Air::parse(air, air_len).log_quotient_degree(public_degree);
+    });
+}
+
+int lsp_quotient_values(lsp_ctx* ctx, const lsp_fr* lde, size_t h, size_t w, const int32_t* air, size_t air_len,
+                        const lsp_fr* pubv, size_t npub, const lsp_fr* alpha, lsp_fr* out, int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && alpha && pubv && npub >= 2, LSP_E_ARG, "bad quotient arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const Air A = Air::parse(air, air_len);
+        LSP_REQUIRE(A.max_col < w, LSP_E_ARG, "AIR column outside width");
+        const uint32_t log_h = log2_exact(h), log_q = A.log_quotient_degree(ctx->public_degree);
+        const uint32_t logQ = log_h + log_q;
+        LSP_REQUIRE(log_q <= ctx->log_blowup, LSP_E_ARG, "quotient degree exceeds blowup");
+        const size_t N = h << ctx->log_blowup, Q = (size_t)1 << logQ, q = (size_t)1 << log_q;
+        const Fr* dlde = dev_in(ctx, lde, N * w, mem, "api_in");
+        Fr* dout = dev_out(ctx, out, Q, mem, "api_out");
+        const Fr GEN = host_generator(), one = fr_one();
+        const Fr wh_inv = fr_inv(host_two_adic_generator(log_h));
+        uint32_t L1 = (logQ + 1) / 2, L2 = logQ - L1;
+        Fr* tab = ctx->fbuf("api_tab", (1ull << L1) + (1ull << L2));
+        Fr* b = ctx->fbuf("api_tab_base", 1);
+        const Fr gq = host_two_adic_generator(logQ);
+        LSP_HIP(hipMemcpyAsync(b, &gq, sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+        LSP_HIP(launch_pow_tables(b, 1, L1, L2, nullptr, tab, ctx->stream));
+        Fr* den = ctx->fbuf("q_den", Q);
+        Fr* inv_den = ctx->fbuf("q_invden", Q);
+        LSP_HIP(launch_selector_denoms(tab, L1, GEN, wh_inv, Q, den, ctx->stream));
+        LSP_HIP(launch_batch_inverse(den, inv_den, Q, ctx->stream));
+        std::vector<Fr> zz(2 * q);
+        const Fr gh = fr_pow_u64(GEN, h), gl = host_two_adic_generator(log_q);
+        Fr gg = one;
+        for (size_t k = 0; k < q; ++k) {
+            zz[k] = fr_sub(fr_mul(gh, gg), one);
+            zz[q + k] = fr_inv(zz[k]);
+            gg = fr_mul(gg, gl);
+        }
+        Fr* dz = ctx->fbuf("q_zh", 2 * q);
+        LSP_HIP(hipMemcpyAsync(dz, zz.data(), zz.size() * sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+        int32_t* dair = (int32_t*)ctx->buf("air", A.raw.size() * sizeof(int32_t));
+        LSP_HIP(hipMemcpyAsync(dair, A.raw.data(), A.raw.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                               ctx->stream));
+        QuotientArgs qa;
+        qa.lde = dlde;
+        qa.w = (uint32_t)w;
+        qa.logQ = logQ;
+        qa.log_q = log_q;
+        qa.air = dair;
+        qa.air_len = (uint32_t)A.raw.size();
+        qa.pub_alpha = to_fr(pubv[0]);
+        qa.pub_delta = to_fr(pubv[1]);
+        qa.alpha = to_fr(*alpha);
+        qa.gen = GEN;
+        qa.wh_inv = wh_inv;
+        qa.tabQ = tab;
+        qa.L1 = L1;
+        qa.zh = dz;
+        qa.inv_zh = dz + q;
+        qa.inv_den = inv_den;
+        qa.out = dout;
+        LSP_HIP(launch_quotient(qa, ctx->stream));
+        finish_out(ctx, out, dout, Q, mem);
+    });
+}
+
+int lsp_interpolate_coset(lsp_ctx* ctx, const lsp_fr* lde_bitrev, size_t h, size_t w, const lsp_fr* shift,
+                          const lsp_fr* z, lsp_fr* ys_out, int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && shift && z && ys_out && w >= 1, LSP_E_ARG, "bad interpolate arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const uint32_t logh = log2_exact(h);
+        const Fr* dm = dev_in(ctx, lde_bitrev, h * w, mem, "api_in");
+        const Fr S = to_fr(*shift), Z = to_fr(*z);
+        uint32_t L1 = (logh + 1) / 2, L2 = logh - L1;
+        Fr* tab = ctx->fbuf("api_tab", (1ull << L1) + (1ull << L2));
+        Fr* b = ctx->fbuf("api_tab_base", 1);
+        const Fr gh = host_two_adic_generator(logh);
+        LSP_HIP(hipMemcpyAsync(b, &gh, sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+        LSP_HIP(launch_pow_tables(b, 1, L1, L2, nullptr, tab, ctx->stream));
+        Fr* den = ctx->fbuf("o_den", h);
+        Fr* inv = ctx->fbuf("o_invz", h);
+        LSP_HIP(launch_open_denoms(Z, S, tab, L1, logh, h, den, ctx->stream));
+        LSP_HIP(launch_batch_inverse(den, inv, h, ctx->stream));
+        Fr* partial = ctx->fbuf("o_partial", ((h + 1023) / 1024) * w);
+        Fr* sums = ctx->fbuf("o_sums", w);
+        uint32_t nb = 0;
+        LSP_HIP(launch_interp_partial(dm, (uint32_t)w, h, inv, S, tab, L1, logh, partial, &nb, ctx->stream));
+        LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)w, sums, ctx->stream));
+        std::vector<Fr> hs(w);
+        LSP_HIP(hipMemcpyAsync(hs.data(), sums, w * sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+        ctx->sync();
+        const Fr sh = fr_pow_u64(S, h);
+        const Fr f = fr_mul(fr_sub(fr_pow_u64(Z, h), sh), fr_inv(fr_mul(sh, fr_from_u64(h))));
+        for (size_t c = 0; c < w; ++c) ys_out[c] = from_fr(fr_mul(hs[c], f));
+    });
+}
+
+int lsp_batch_inverse(lsp_ctx* ctx, const lsp_fr* in, size_t n, lsp_fr* out, int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx, LSP_E_ARG, "null ctx");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const Fr* din = dev_in(ctx, in, n, mem, "api_in");
+        Fr* dout = dev_out(ctx, out, n, mem, "api_out");
+        LSP_REQUIRE(din != dout, LSP_E_ARG, "batch_inverse cannot run in place");
+        LSP_HIP(launch_batch_inverse(din, dout, n, ctx->stream));
+        finish_out(ctx, out, dout, n, mem);
+    });
+}
+
+int lsp_prove(lsp_ctx* ctx, const lsp_fr* trace, size_t h, size_t w, const int32_t* air, size_t air_len,
+              const lsp_fr* pubv, size_t npub, int mem, lsp_proof** out) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && out && pubv, LSP_E_ARG, "bad prove arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const Air A = Air::parse(air, air_len);
+        std::vector<Fr> pub(npub);
+        for (size_t i = 0; i < npub; ++i) pub[i] = to_fr(pubv[i]);
+        const Fr* din = dev_in(ctx, trace, h * w, mem, "trace_in");
+        *out = prove_device(ctx, din, h, w, A, pub.data(), npub);
+    });
+}
+
+int lsp_proof_serialize(const lsp_proof* p, uint8_t* buf, size_t cap, size_t* len) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(p && len, LSP_E_ARG, "null");
+        const std::vector<uint8_t> b = serialize(*p);
+        *len = b.size();
+        if (buf) {
+            LSP_REQUIRE(cap >= b.size(), LSP_E_ARG, "buffer too small");
+            std::memcpy(buf, b.data(), b.size());
+        }
+    });
+}
+
+int lsp_proof_free(lsp_proof* p) {
+    delete p;
+    return LSP_OK;
+}
+
+int lsp_verify(const lsp_ctx* ctx, const int32_t* air, size_t air_len, const lsp_fr* pubv, size_t npub,
+               const uint8_t* proof, size_t len) {
+    int rc = LSP_OK;
+    int g = guarded(nullptr, [&] {
+        LSP_REQUIRE(ctx && pubv && proof, LSP_E_ARG, "bad verify arguments");
+        const Air A = Air::parse(air, air_len);
+        std::vector<Fr> pub(npub);
+        for (size_t i = 0; i < npub; ++i) pub[i] = to_fr(pubv[i]);
+        const int v = verify_host(ctx, A, pub.data(), npub, proof, len);
+        if (v != 0) {
+            g_err = "proof rejected at check " + std::to_string(v);
+            rc = LSP_E_VERIFY;
+        }
+    });
+    return g != LSP_OK ? g : rc;
+}
+
+int lsp_last_timings(const lsp_ctx* ctx, double* ms, const char** names, size_t cap, size_t* n) {
+    if (!ctx || !n) return LSP_E_ARG;
+    *n = ctx->timings.size();
+    for (size_t i = 0; i < ctx->timings.size() && i < cap; ++i) {
+        if (ms) ms[i] = ctx->timings[i].second;
+        if (names) names[i] = ctx->timings[i].first.c_str();
+    }
+    return LSP_OK;
+}
+
+int lsp_gen_permutation_trace(uint64_t seed, uint32_t log_n, uint32_t ncols, const lsp_fr* alpha,
+                              const lsp_fr* delta, int small_values, lsp_fr* rows) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(alpha && delta && rows && ncols >= 1 && log_n >= 1 && log_n <= 30, LSP_E_ARG,
+                    "bad trace arguments");
+        const size_t n = (size_t)1 << log_n, w = 2 * (size_t)ncols + 2;
+        SplitMix64 g{seed ^ 0x5452414345ull};  // "TRACE"
+        std::vector<Fr> a((size_t)ncols * n);
+        for (uint32_t c = 0; c < ncols; ++c)
+            for (size_t i = 0; i < n; ++i)
+                a[c * n + i] = small_values ? fr_from_u64(g.next() & 0xFFFFFFFFull) : g.fr();
+        std::vector<size_t> perm(n);
+        for (size_t i = 0; i < n; ++i) perm[i] = i;
+        for (size_t i = n - 1; i > 0; --i) std::swap(perm[i], perm[g.below(i + 1)]);
+        const Fr al = to_fr(*alpha), dl = to_fr(*delta);
+        std::vector<Fr> den(n), inv(n);
+        for (size_t i = 0; i < n; ++i) {
+            Fr bc = fr_zero();
+            for (uint32_t c = 0; c < ncols; ++c) bc = fr_add(fr_mul(bc, al), a[c * n + perm[i]]);
+            den[i] = fr_add(bc, dl);
+        }
+        // batch inverse (RawPermutationTrace::get_trace inverts per row; same values)
+        Fr acc = fr_one();
+        for (size_t i = 0; i < n; ++i) {
+            inv[i] = acc;
+            acc = fr_mul(acc, den[i]);
+        }
+        Fr ia = fr_inv(acc);
+        for (size_t i = n; i-- > 0;) {
+            const Fr t = fr_mul(ia, inv[i]);
+            ia = fr_mul(ia, den[i]);
+            inv[i] = t;
+        }
+        Fr prev = fr_one();
+        for (size_t i = 0; i < n; ++i) {
+            Fr* row = reinterpret_cast<Fr*>(rows) + i * w;
+            Fr ac = fr_zero();
+            for (uint32_t c = 0; c < ncols; ++c) {
+                row[c] = a[c * n + i];
+                row[ncols + c] = a[c * n + perm[i]];
+                ac = fr_add(fr_mul(ac, al), row[c]);
+            }
+            row[2 * ncols] = inv[i];
+            prev = fr_mul(fr_mul(prev, fr_add(ac, dl)), inv[i]);
+            row[2 * ncols + 1] = prev;
+        }
+        LSP_REQUIRE(fr_eq(prev, fr_one()), LSP_E_STATE,
+                    "failed to check constrain: check column should be 1 on the last row");
+    });
+}
+
+}  // extern "C"

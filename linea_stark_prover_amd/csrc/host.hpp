@@ -1,0 +1,173 @@
+// Host-side internals of liblsp_hip.so: context, device buffer pool,
+// transcript (HashChallenger), proof object.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/lsp.h"
+#include "fr.hpp"
+#include "kernels.hpp"
+#include "poseidon2.hpp"
+
+namespace lsp {
+
+struct LspError : std::runtime_error {
+    int code;
+    LspError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define LSP_HIP(x)                                                                                  \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess)                                                                       \
+            throw ::lsp::LspError(LSP_E_HIP, std::string(#x) + " -> " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define LSP_REQUIRE(cond, code, msg)                          \
+    do {                                                      \
+        if (!(cond)) throw ::lsp::LspError((code), (msg));    \
+    } while (0)
+
+inline Fr to_fr(const lsp_fr& x) {
+    Fr r;
+    for (int i = 0; i < 4; ++i) {
+        r.v[2 * i] = (uint32_t)x.l[i];
+        r.v[2 * i + 1] = (uint32_t)(x.l[i] >> 32);
+    }
+    return r;
+}
+inline lsp_fr from_fr(const Fr& x) {
+    lsp_fr r;
+    for (int i = 0; i < 4; ++i) r.l[i] = (uint64_t)x.v[2 * i] | ((uint64_t)x.v[2 * i + 1] << 32);
+    return r;
+}
+
+// GENERATOR = 22 (U9) and two-adic generators
+Fr host_generator();
+Fr host_two_adic_generator(uint32_t bits);
+uint64_t host_bitrev(uint64_t x, uint32_t bits);
+uint32_t log2_exact(size_t n);  // throws LSP_E_SIZE on non-power-of-two
+
+struct P2Host {
+    P2Layout L;
+    std::vector<Fr> rc;
+    void permute(Fr& s0, Fr& s1, Fr& s2) const { permute3_rt(s0, s1, s2, rc.data(), L); }
+    Fr hash(const Fr* in, size_t n) const;
+    Fr compress(const Fr& l, const Fr& r) const {
+        Fr s0 = l, s1 = r, s2 = fr_zero();
+        permute(s0, s1, s2);
+        return s0;
+    }
+};
+
+// HashChallenger<Val, Hash, 1> (bin/src/config.rs:23): input buffer,
+// output buffer, hash_iter on flush with the output chained back as input.
+struct Challenger {
+    const P2Host* p2;
+    std::vector<Fr> in, out;
+    explicit Challenger(const P2Host* p) : p2(p) {}
+    void observe(const Fr& x) {
+        out.clear();
+        in.push_back(x);
+    }
+    Fr sample() {
+        if (out.empty()) {
+            Fr h = p2->hash(in.data(), in.size());
+            in.assign(1, h);
+            out.assign(1, h);
+        }
+        Fr r = out.back();
+        out.pop_back();
+        return r;
+    }
+    // U8: low bits of the canonical value
+    uint64_t sample_bits(uint32_t bits) {
+        Fr c = fr_to_canonical(sample());
+        uint64_t lo = (uint64_t)c.v[0] | ((uint64_t)c.v[1] << 32);
+        return bits >= 64 ? lo : (lo & ((1ull << bits) - 1));
+    }
+    bool check_witness(uint32_t bits, uint64_t w) {
+        observe(fr_from_u64(w));
+        return sample_bits(bits) == 0;
+    }
+    uint64_t grind(uint32_t bits) {
+        for (uint64_t w = 0;; ++w) {
+            Challenger probe = *this;
+            if (probe.check_witness(bits, w)) {
+                check_witness(bits, w);
+                return w;
+            }
+        }
+    }
+};
+
+struct AirCfg {
+    int type;  // 1 perm, 2 lookup
+    std::vector<int32_t> a, b;             // perm: a, b ; lookup: a, flattened b tables
+    int32_t binv = 0, check = 0;           // perm
+    int32_t ntab = 0, nbc = 0, a_filter = 0, a_inv = 0;
+    std::vector<int32_t> b_filter, b_inv, occ;
+};
+struct Air {
+    std::vector<AirCfg> cfgs;
+    std::vector<int32_t> raw;
+    uint32_t max_col = 0;
+    static Air parse(const int32_t* d, size_t n);
+    // (max constraint degree, constraint count) under the U6 public-degree rule
+    std::pair<int, int> stats(int public_degree) const;
+    uint32_t log_quotient_degree(int public_degree) const;
+    // concrete evaluation folded into acc (verifier / tests)
+    void eval_fold(const Fr* loc, const Fr* nxt, const Fr& ap, const Fr& dl, const Fr& first, const Fr& last,
+                   const Fr& trans, const Fr& alpha, Fr& acc) const;
+};
+
+struct lsp_query {
+    std::vector<Fr> trow, tpath, qrow, qpath, sib;
+    std::vector<std::vector<Fr>> fpath;
+};
+
+}  // namespace lsp
+
+struct lsp_proof {
+    uint32_t log_h = 0, log_q = 0, w = 0;
+    lsp::Fr troot, qroot, pow_w;
+    std::vector<lsp::Fr> tl, tn, qc, roots, final_poly;
+    std::vector<lsp::lsp_query> queries;
+};
+
+struct lsp_tree {
+    lsp_ctx* ctx = nullptr;
+    size_t height = 0;
+    std::vector<size_t> widths;
+    lsp::Fr* layers = nullptr;         // device, 2*height - 1
+    std::vector<lsp::Fr*> mats;        // device copies (owned) of the committed matrices
+};
+
+struct lsp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    lsp::P2Host p2;
+    lsp::Fr* rc_dev = nullptr;
+    uint32_t log_blowup = 3, log_final_poly_len = 0, num_queries = 33, pow_bits = 0;
+    int32_t public_degree = 1;
+    std::string err;
+    std::mutex mu;
+    struct Buf {
+        void* p = nullptr;
+        size_t cap = 0;
+    };
+    std::map<std::string, Buf> pool;
+    std::map<std::pair<uint32_t, int>, lsp::Fr*> twiddles;
+    std::vector<std::pair<std::string, double>> timings;
+
+    void* buf(const std::string& name, size_t bytes);
+    lsp::Fr* fbuf(const std::string& name, size_t n) { return (lsp::Fr*)buf(name, n * sizeof(lsp::Fr)); }
+    const lsp::Fr* twiddle(uint32_t logH, bool inverse);
+    void sync();
+};

@@ -1,0 +1,53 @@
+// Batch inversion (p3-field batch_multiplicative_inverse) and the gather used
+// to pull query openings off the device in one copy.
+#include "k_common.hpp"
+#include "kernels.hpp"
+
+namespace lsp {
+
+namespace {
+constexpr uint32_t BINV_CHUNK = 32;  // elements per thread: 1 Fermat inverse per 32 elements
+
+// Thread t owns elements t, t+T, t+2T, ... (interleaved so every pass is coalesced)
+__global__ __launch_bounds__(256) void k_batch_inverse(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n,
+                                                       size_t T) {
+    const size_t t = gtid();
+    if (t >= T) return;
+    Fr acc = fr_one();
+    uint32_t cnt = 0;
+    for (uint32_t j = 0; j < BINV_CHUNK; ++j) {
+        const size_t i = t + (size_t)j * T;
+        if (i >= n) break;
+        out[i] = acc;
+        acc = fr_mul(acc, in[i]);
+        ++cnt;
+    }
+    Fr inv = fr_inv(acc);
+    for (uint32_t j = cnt; j-- > 0;) {
+        const size_t i = t + (size_t)j * T;
+        const Fr o = fr_mul(inv, out[i]);
+        inv = fr_mul(inv, in[i]);
+        out[i] = o;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gather(const uint64_t* __restrict__ ptrs, Fr* __restrict__ out, size_t n) {
+    const size_t i = gtid();
+    if (i < n) out[i] = *reinterpret_cast<const Fr*>(ptrs[i]);
+}
+}  // namespace
+
+hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st) {
+    if (!n) return hipSuccess;
+    const size_t T = (n + BINV_CHUNK - 1) / BINV_CHUNK;
+    hipLaunchKernelGGL(k_batch_inverse, dim3(nblocks(T, 256)), dim3(256), 0, st, in, out, n, T);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather(const uint64_t* ptrs, Fr* out, size_t n, hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_gather, dim3(nblocks(n, 256)), dim3(256), 0, st, ptrs, out, n);
+    return hipGetLastError();
+}
+
+}  // namespace lsp

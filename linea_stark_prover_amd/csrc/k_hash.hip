@@ -1,0 +1,136 @@
+// Poseidon2-w3 permutation batches, row hashing (PaddingFreeSponge) and
+// Merkle levels (CompressionFunctionFromHasher) -- the kernels behind
+// MerkleTreeMmcs::commit ([EXT p3-merkle-tree], bin/src/config.rs:19-20).
+//
+// One thread owns one permutation state (3 x 8 VGPRs); the work is integer
+// VALU bound (~230 Montgomery products per permutation), so the kernels are
+// plain one-state-per-lane loops with the round constants on the scalar path
+// (uniform addresses -> s_load).
+#include "k_common.hpp"
+#include "kernels.hpp"
+
+namespace lsp {
+
+namespace {
+template <uint32_t D>
+__global__ __launch_bounds__(256) void k_permute(Fr* __restrict__ st, size_t n, const Fr* __restrict__ rc,
+                                                 uint32_t rf, uint32_t rp) {
+    const size_t i = gtid();
+    if (i >= n) return;
+    Fr s0 = st[3 * i], s1 = st[3 * i + 1], s2 = st[3 * i + 2];
+    permute3<D>(s0, s1, s2, rc, rf, rp);
+    st[3 * i] = s0;
+    st[3 * i + 1] = s1;
+    st[3 * i + 2] = s2;
+}
+
+template <uint32_t D>
+__global__ __launch_bounds__(256) void k_hash_rows1(const Fr* __restrict__ m, uint32_t w, size_t nrows,
+                                                    Fr* __restrict__ out, const Fr* __restrict__ rc, uint32_t rf,
+                                                    uint32_t rp) {
+    const size_t i = gtid();
+    if (i >= nrows) return;
+    const Fr* row = m + i * w;
+    out[i] = sponge<D>([&](uint32_t k) { return row[k]; }, w, rc, rf, rp);
+}
+
+template <uint32_t D>
+__global__ __launch_bounds__(256) void k_hash_rows_multi(MatList ml, size_t nrows, Fr* __restrict__ out,
+                                                         const Fr* __restrict__ rc, uint32_t rf, uint32_t rp) {
+    const size_t i = gtid();
+    if (i >= nrows) return;
+    uint32_t total = 0;
+    for (uint32_t j = 0; j < ml.n; ++j) total += ml.width[j];
+    auto get = [&](uint32_t k) {
+        uint32_t j = 0;
+        while (k >= ml.width[j]) {
+            k -= ml.width[j];
+            ++j;
+        }
+        return ml.ptr[j][i * ml.width[j] + k];
+    };
+    out[i] = sponge<D>(get, total, rc, rf, rp);
+}
+
+template <uint32_t D>
+__global__ __launch_bounds__(256) void k_merkle_level(const Fr* __restrict__ src, Fr* __restrict__ dst, size_t nout,
+                                                      const Fr* __restrict__ rc, uint32_t rf, uint32_t rp) {
+    const size_t i = gtid();
+    if (i >= nout) return;
+    dst[i] = compress2<D>(src[2 * i], src[2 * i + 1], rc, rf, rp);
+}
+
+// Top of a tree in one workgroup: `len` (<= 1024, power of two) digests at
+// layers[off..off+len) -> every layer above them, through the LDS.
+template <uint32_t D>
+__global__ __launch_bounds__(512) void k_merkle_top(Fr* __restrict__ layers, size_t off, uint32_t len,
+                                                    const Fr* __restrict__ rc, uint32_t rf, uint32_t rp) {
+    __shared__ Fr buf[1024];
+    for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) buf[e] = layers[off + e];
+    __syncthreads();
+    size_t out_off = off + len;
+    while (len > 1) {
+        const uint32_t nout = len / 2;
+        Fr r;
+        if (threadIdx.x < nout) r = compress2<D>(buf[2 * threadIdx.x], buf[2 * threadIdx.x + 1], rc, rf, rp);
+        __syncthreads();
+        if (threadIdx.x < nout) {
+            buf[threadIdx.x] = r;
+            layers[out_off + threadIdx.x] = r;
+        }
+        __syncthreads();
+        out_off += nout;
+        len = nout;
+    }
+}
+}  // namespace
+
+#define LSP_DISPATCH_D(L, KERNEL, ...)                                  \
+    do {                                                                \
+        if ((L).sbox_degree == 17)                                      \
+            hipLaunchKernelGGL(KERNEL<17>, __VA_ARGS__);                \
+        else                                                            \
+            hipLaunchKernelGGL(KERNEL<11>, __VA_ARGS__);                \
+    } while (0)
+
+hipError_t launch_permute(Fr* states, size_t n, const Fr* rc, P2Layout L, hipStream_t st) {
+    if (!n) return hipSuccess;
+    LSP_DISPATCH_D(L, k_permute, dim3(nblocks(n, 256)), dim3(256), 0, st, states, n, rc, L.rounds_f, L.rounds_p);
+    return hipGetLastError();
+}
+
+hipError_t launch_hash_rows(const MatList& m, size_t nrows, Fr* out, const Fr* rc, P2Layout L, hipStream_t st) {
+    if (!nrows) return hipSuccess;
+    if (m.n == 1)
+        LSP_DISPATCH_D(L, k_hash_rows1, dim3(nblocks(nrows, 256)), dim3(256), 0, st, m.ptr[0], m.width[0], nrows,
+                       out, rc, L.rounds_f, L.rounds_p);
+    else
+        LSP_DISPATCH_D(L, k_hash_rows_multi, dim3(nblocks(nrows, 256)), dim3(256), 0, st, m, nrows, out, rc,
+                       L.rounds_f, L.rounds_p);
+    return hipGetLastError();
+}
+
+hipError_t launch_merkle_level(const Fr* src, Fr* dst, size_t nout, const Fr* rc, P2Layout L, hipStream_t st) {
+    if (!nout) return hipSuccess;
+    LSP_DISPATCH_D(L, k_merkle_level, dim3(nblocks(nout, 256)), dim3(256), 0, st, src, dst, nout, rc, L.rounds_f,
+                   L.rounds_p);
+    return hipGetLastError();
+}
+
+hipError_t launch_merkle_tree(Fr* layers, size_t nleaves, const Fr* rc, P2Layout L, hipStream_t st) {
+    size_t off = 0, len = nleaves;
+    while (len > 1024) {
+        hipError_t e = launch_merkle_level(layers + off, layers + off + len, len / 2, rc, L, st);
+        if (e != hipSuccess) return e;
+        off += len;
+        len /= 2;
+    }
+    if (len > 1) {
+        LSP_DISPATCH_D(L, k_merkle_top, dim3(1), dim3(512), 0, st, layers, off, (uint32_t)len, rc, L.rounds_f,
+                       L.rounds_p);
+        return hipGetLastError();
+    }
+    return hipSuccess;
+}
+
+}  // namespace lsp

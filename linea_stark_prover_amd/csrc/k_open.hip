@@ -1,0 +1,118 @@
+// TwoAdicFriPcs::open building blocks ([EXT p3-fri]): inverse denominators
+// 1/(z - GEN w_N^bitrev(i)), barycentric opened values (interpolate_coset),
+// the "reduce rows" accumulation, and the FRI fold
+// (TwoAdicFriGenericConfig::fold_matrix).
+#include "k_common.hpp"
+#include "kernels.hpp"
+
+namespace lsp {
+
+namespace {
+__global__ __launch_bounds__(256) void k_open_denoms(Fr z, Fr gen, const Fr* __restrict__ tabN, uint32_t L1,
+                                                     uint32_t logN, size_t n, Fr* __restrict__ den) {
+    const size_t i = gtid();
+    if (i >= n) return;
+    den[i] = fr_sub(z, fr_mul(gen, pow2l(tabN, L1, brev_bits(i, logN))));
+}
+
+constexpr uint32_t INTERP_ROWS = 1024;  // rows per block
+
+// partial[b*w + c] = sum over the block's rows i of M[i][c] * x_i * inv_den[i]
+__global__ __launch_bounds__(256) void k_interp_partial(const Fr* __restrict__ M, uint32_t w, size_t h,
+                                                        const Fr* __restrict__ inv_den, Fr gen,
+                                                        const Fr* __restrict__ tabN, uint32_t L1, uint32_t logN,
+                                                        Fr* __restrict__ partial) {
+    __shared__ Fr red[256];
+    __shared__ Fr sc[INTERP_ROWS];
+    const size_t r0 = (size_t)blockIdx.x * INTERP_ROWS;
+    for (uint32_t e = threadIdx.x; e < INTERP_ROWS; e += blockDim.x) {
+        const size_t i = r0 + e;
+        if (i < h) sc[e] = fr_mul(fr_mul(gen, pow2l(tabN, L1, brev_bits(i, logN))), inv_den[i]);
+    }
+    __syncthreads();
+    for (uint32_t c = 0; c < w; ++c) {
+        Fr acc = fr_zero();
+        for (uint32_t e = threadIdx.x; e < INTERP_ROWS; e += blockDim.x) {
+            const size_t i = r0 + e;
+            if (i < h) acc = fr_add(acc, fr_mul(M[i * w + c], sc[e]));
+        }
+        red[threadIdx.x] = acc;
+        __syncthreads();
+        for (uint32_t s = 128; s > 0; s >>= 1) {
+            if (threadIdx.x < s) red[threadIdx.x] = fr_add(red[threadIdx.x], red[threadIdx.x + s]);
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) partial[(size_t)blockIdx.x * w + c] = red[0];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sum_partials(const Fr* __restrict__ partial, uint32_t nb, uint32_t w,
+                                                      Fr* __restrict__ out) {
+    const size_t c = gtid();
+    if (c >= w) return;
+    Fr acc = fr_zero();
+    for (uint32_t b = 0; b < nb; ++b) acc = fr_add(acc, partial[(size_t)b * w + c]);
+    out[c] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_reduce_rows(ReduceArgs a) {
+    const size_t i = gtid();
+    if (i >= a.n) return;
+    const Fr* row = a.lde + i * a.w;
+    Fr rr = fr_zero();
+    for (uint32_t k = 0; k < a.w; ++k) rr = fr_add(rr, fr_mul(a.apw[k], row[k]));
+    const Fr iz = a.inv_z[i];
+    Fr acc = fr_mul(fr_sub(a.ry_z, rr), iz);
+    acc = fr_add(acc, fr_mul(fr_mul(fr_sub(a.ry_zn, rr), a.inv_zn[i]), a.apw[a.w]));
+    const Fr* qrow = a.qlde + i * a.q;
+    Fr qacc = fr_zero();
+    for (uint32_t j = 0; j < a.q; ++j) qacc = fr_add(qacc, fr_mul(a.apw[2 * a.w + j], fr_sub(a.ryq[j], qrow[j])));
+    acc = fr_add(acc, fr_mul(qacc, iz));
+    a.out[i] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_fri_fold(const Fr* __restrict__ v, size_t m, Fr half, Fr half_beta,
+                                                  const Fr* __restrict__ tab, uint32_t L1, uint32_t logm,
+                                                  Fr* __restrict__ out) {
+    const size_t i = gtid();
+    if (i >= m) return;
+    const Fr p = fr_mul(half_beta, pow2l(tab, L1, brev_bits(i, logm)));
+    out[i] = fr_add(fr_mul(fr_add(half, p), v[2 * i]), fr_mul(fr_sub(half, p), v[2 * i + 1]));
+}
+}  // namespace
+
+hipError_t launch_open_denoms(Fr z, Fr gen, const Fr* tabN, uint32_t L1, uint32_t logN, size_t n, Fr* den,
+                              hipStream_t st) {
+    hipLaunchKernelGGL(k_open_denoms, dim3(nblocks(n, 256)), dim3(256), 0, st, z, gen, tabN, L1, logN, n, den);
+    return hipGetLastError();
+}
+
+hipError_t launch_interp_partial(const Fr* M, uint32_t w, size_t h, const Fr* inv_den, Fr gen, const Fr* tabN,
+                                 uint32_t L1, uint32_t logN, Fr* partial, uint32_t* nb, hipStream_t st) {
+    *nb = (uint32_t)((h + INTERP_ROWS - 1) / INTERP_ROWS);
+    hipLaunchKernelGGL(k_interp_partial, dim3(*nb), dim3(256), 0, st, M, w, h, inv_den, gen, tabN, L1, logN,
+                       partial);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum_partials(const Fr* partial, uint32_t nb, uint32_t w, Fr* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_sum_partials, dim3(nblocks(w, 256)), dim3(256), 0, st, partial, nb, w, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce_rows(const ReduceArgs& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_reduce_rows, dim3(nblocks(a.n, 256)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fri_fold(const Fr* v, size_t m, Fr half, Fr half_beta, const Fr* tab, uint32_t L1, Fr* out,
+                           hipStream_t st) {
+    uint32_t logm = 0;
+    while ((1ull << logm) < m) ++logm;
+    hipLaunchKernelGGL(k_fri_fold, dim3(nblocks(m, 256)), dim3(256), 0, st, v, m, half, half_beta, tab, L1, logm,
+                       out);
+    return hipGetLastError();
+}
+
+}  // namespace lsp

@@ -1,0 +1,103 @@
+// Device kernels of the hot path and their host launchers.
+// Each launcher enqueues on `st` and returns hipError_t of the launch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "fr.hpp"
+#include "poseidon2.hpp"
+
+namespace lsp {
+
+// ------------------------------------------------------------ k_ntt.hip
+// dst[b][c][r] = src[b][rp(r)][c]; src is batch x R x C row-major,
+// rp = bit reversal over log2(R) bits when bitrev_rows, identity otherwise.
+hipError_t launch_transpose(const Fr* src, Fr* dst, size_t batch, size_t R, size_t C, bool bitrev_rows,
+                            hipStream_t st);
+// In-place radix-2 NTT over `batch` contiguous arrays of 2^logH elements.
+// dif=true : natural in -> bit-reversed out, twiddles tw[x] = w^x (x < H/2)
+// dif=false: bit-reversed in -> natural out (DIT)
+hipError_t launch_ntt(Fr* data, size_t batch, uint32_t logH, const Fr* tw, bool dif, hipStream_t st);
+// Two-level power tables: for each base b,
+// tab[b] = {b^j, j < 2^L1} ++ {b^(j 2^L1) * scale[b], j < 2^L2}   (scale nullable)
+hipError_t launch_pow_tables(const Fr* bases, size_t nbases, uint32_t L1, uint32_t L2, const Fr* scale,
+                             Fr* tabs, hipStream_t st);
+// out[i] = base^i for i < n, from a two-level table of base
+hipError_t launch_powers(const Fr* tab, uint32_t L1, size_t n, Fr* out, hipStream_t st);
+// Y[(k*w + c)*h + i] = X[c*h + i] * pow2l(tab_{k*w+c}, i); the inverse transform's
+// 1/h is folded into the tables' scale
+hipError_t launch_twist_expand(const Fr* X, Fr* Y, size_t w, uint32_t logh, uint32_t ncosets, const Fr* tabs,
+                               uint32_t L1, uint32_t L2, hipStream_t st);
+
+// ----------------------------------------------------------- k_hash.hip
+struct MatList {
+    const Fr* ptr[8];
+    uint32_t width[8];
+    uint32_t n;
+};
+hipError_t launch_permute(Fr* states, size_t n, const Fr* rc, P2Layout L, hipStream_t st);
+// out[i] = hash_iter(concat of row i of every matrix in `m`)
+hipError_t launch_hash_rows(const MatList& m, size_t nrows, Fr* out, const Fr* rc, P2Layout L, hipStream_t st);
+// dst[i] = compress(src[2i], src[2i+1]) for i < nout
+hipError_t launch_merkle_level(const Fr* src, Fr* dst, size_t nout, const Fr* rc, P2Layout L, hipStream_t st);
+// full tree above the leaf digests already stored at layers[0..nleaves)
+hipError_t launch_merkle_tree(Fr* layers, size_t nleaves, const Fr* rc, P2Layout L, hipStream_t st);
+
+// --------------------------------------------------------- k_field.hip
+// out[i] = 1 / in[i] (Montgomery trick, interleaved chunks); in may alias out? no
+hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st);
+// out[i] = *ptrs[i]
+hipError_t launch_gather(const uint64_t* ptrs, Fr* out, size_t n, hipStream_t st);
+
+// ----------------------------------------------------- k_quotient.hip
+struct QuotientArgs {
+    const Fr* lde;      // N x w row-major, bit-reversed LDE
+    uint32_t w;
+    uint32_t logQ, log_q;
+    const int32_t* air; // device copy of the AIR descriptor
+    uint32_t air_len;
+    Fr pub_alpha, pub_delta, alpha;
+    Fr gen;             // coset shift GEN
+    Fr wh_inv;          // w_h^-1 (last row point)
+    const Fr* tabQ;     // two-level table of w_Q
+    uint32_t L1;
+    const Fr* zh;       // q values of Z_H on the coset (index i mod q)
+    const Fr* inv_zh;   // their inverses
+    const Fr* inv_den;  // 1/((x-1)(x-w_h^-1)) per point
+    Fr* out;            // Q values
+};
+// den[i] = (x_i - 1)(x_i - w_h^-1), x_i = GEN * w_Q^i
+hipError_t launch_selector_denoms(const Fr* tabQ, uint32_t L1, Fr gen, Fr wh_inv, size_t Q, Fr* den,
+                                  hipStream_t st);
+hipError_t launch_quotient(const QuotientArgs& a, hipStream_t st);
+
+// --------------------------------------------------------- k_open.hip
+// den[i] = z - GEN * w_N^bitrev(i) for i < n (two-level table of w_N)
+hipError_t launch_open_denoms(Fr z, Fr gen, const Fr* tabN, uint32_t L1, uint32_t logN, size_t n, Fr* den,
+                              hipStream_t st);
+// partial sums for barycentric interpolation over rows [0, h):
+// partial[b*w + c] = sum_{i in block b} M[i][c] * x_i * inv_den[i]
+hipError_t launch_interp_partial(const Fr* M, uint32_t w, size_t h, const Fr* inv_den, Fr gen, const Fr* tabN,
+                                 uint32_t L1, uint32_t logN, Fr* partial, uint32_t* nblocks, hipStream_t st);
+// out[c] = sum_b partial[b*w + c]
+hipError_t launch_sum_partials(const Fr* partial, uint32_t nblocks, uint32_t w, Fr* out, hipStream_t st);
+struct ReduceArgs {
+    const Fr* lde;  // N x w
+    uint32_t w;
+    const Fr* qlde; // N x q
+    uint32_t q;
+    const Fr* inv_z;   // 1/(zeta - x_i)
+    const Fr* inv_zn;  // 1/(zeta_next - x_i)
+    const Fr* apw;     // alpha_fri^k, k < 2w + q
+    Fr ry_z, ry_zn;    // reduced opened values of the trace at zeta / zeta_next
+    const Fr* ryq;     // opened value of each quotient chunk at zeta (q)
+    Fr* out;           // N
+    size_t n;
+};
+hipError_t launch_reduce_rows(const ReduceArgs& a, hipStream_t st);
+// FRI fold of v (2m values) -> out (m values); tab: two-level table of w_{2m}^-1
+hipError_t launch_fri_fold(const Fr* v, size_t m, Fr half, Fr half_beta, const Fr* tab, uint32_t L1,
+                           Fr* out, hipStream_t st);
+
+}  // namespace lsp

@@ -1,0 +1,500 @@
+// Device pipelines (coset LDE, Merkle commit, quotient, open, FRI) and the
+// p3_uni_stark::prove orchestration (bin/src/main.rs:80-86) on one GPU.
+// The Fiat-Shamir transcript stays on the host (a few dozen hashes); every
+// bulk step runs on the device and only roots, opened values and query
+// openings cross PCIe.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+
+#include "host.hpp"
+#include "prove_internal.hpp"
+
+namespace lsp {
+
+namespace {
+struct PhaseTimer {
+    lsp_ctx* ctx;
+    std::vector<std::pair<std::string, hipEvent_t>> starts;
+    std::vector<std::tuple<std::string, hipEvent_t, hipEvent_t>> done;
+    explicit PhaseTimer(lsp_ctx* c) : ctx(c) {}
+    void begin(const std::string& name) {
+        hipEvent_t e;
+        LSP_HIP(hipEventCreate(&e));
+        LSP_HIP(hipEventRecord(e, ctx->stream));
+        starts.emplace_back(name, e);
+    }
+    void end(const std::string& name) {
+        for (size_t i = starts.size(); i-- > 0;) {
+            if (starts[i].first == name) {
+                hipEvent_t e;
+                LSP_HIP(hipEventCreate(&e));
+                LSP_HIP(hipEventRecord(e, ctx->stream));
+                done.emplace_back(name, starts[i].second, e);
+                starts.erase(starts.begin() + i);
+                return;
+            }
+        }
+    }
+    void collect() {
+        ctx->timings.clear();
+        LSP_HIP(hipStreamSynchronize(ctx->stream));
+        for (auto& t : done) {
+            float ms = 0;
+            LSP_HIP(hipEventElapsedTime(&ms, std::get<1>(t), std::get<2>(t)));
+            ctx->timings.emplace_back(std::get<0>(t), (double)ms);
+            (void)hipEventDestroy(std::get<1>(t));
+            (void)hipEventDestroy(std::get<2>(t));
+        }
+        for (auto& s : starts) (void)hipEventDestroy(s.second);
+        done.clear();
+        starts.clear();
+    }
+};
+
+void two_level(uint32_t bits, uint32_t& L1, uint32_t& L2) {
+    L1 = (bits + 1) / 2;
+    L2 = bits - L1;
+}
+
+// two-level power table of `base` covering exponents < 2^bits, in pool buffer `name`
+const Fr* pow_table(lsp_ctx* ctx, const std::string& name, const Fr& base, uint32_t bits, uint32_t& L1) {
+    uint32_t L2;
+    two_level(bits, L1, L2);
+    Fr* tab = ctx->fbuf(name, (1ull << L1) + (1ull << L2));
+    Fr* b = ctx->fbuf(name + "_base", 1);
+    LSP_HIP(hipMemcpyAsync(b, &base, sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+    LSP_HIP(launch_pow_tables(b, 1, L1, L2, nullptr, tab, ctx->stream));
+    return tab;
+}
+
+Fr d2h_fr(lsp_ctx* ctx, const Fr* d) {
+    Fr x;
+    LSP_HIP(hipMemcpyAsync(&x, d, sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+    LSP_HIP(hipStreamSynchronize(ctx->stream));
+    return x;
+}
+}  // namespace
+
+// ----------------------------------------------------------------- LDE
+void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added_bits, const Fr* shifts_host,
+                Fr* d_out) {
+    const uint32_t logh = log2_exact(h);
+    const uint32_t B = 1u << added_bits;
+    const uint32_t logN = logh + added_bits;
+    LSP_REQUIRE(logN <= 47, LSP_E_SIZE, "LDE larger than the 2-adic subgroup");
+    Fr* X = ctx->fbuf("lde_X", h * w);
+    Fr* Y = ctx->fbuf("lde_Y", h * w * B);
+    hipStream_t st = ctx->stream;
+    // X[c][j] = in[bitrev(j)][c]  (bit-reversed input of the DIT inverse)
+    LSP_HIP(launch_transpose(d_in, X, 1, h, w, true, st));
+    LSP_HIP(launch_ntt(X, w, logh, ctx->twiddle(logh, true), false, st));  // X = h * coefficients
+    // coset k, column c: base s = shift_c * w_N^bitrev_B(k); Y = X * s^i / h
+    const Fr wN = host_two_adic_generator(logN);
+    const Fr hinv = fr_inv(fr_from_u64(h));
+    std::vector<Fr> bases((size_t)B * w), scales((size_t)B * w, hinv);
+    for (uint32_t k = 0; k < B; ++k) {
+        const Fr ck = fr_pow_u64(wN, host_bitrev(k, added_bits));
+        for (size_t c = 0; c < w; ++c) bases[k * w + c] = fr_mul(shifts_host[c], ck);
+    }
+    uint32_t L1, L2;
+    two_level(logh, L1, L2);
+    Fr* dbases = ctx->fbuf("lde_bases", bases.size() * 2);
+    LSP_HIP(hipMemcpyAsync(dbases, bases.data(), bases.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
+    LSP_HIP(hipMemcpyAsync(dbases + bases.size(), scales.data(), scales.size() * sizeof(Fr), hipMemcpyHostToDevice,
+                           st));
+    const size_t per = (1ull << L1) + (1ull << L2);
+    Fr* tabs = ctx->fbuf("lde_tabs", per * bases.size());
+    LSP_HIP(launch_pow_tables(dbases, bases.size(), L1, L2, dbases + bases.size(), tabs, st));
+    LSP_HIP(launch_twist_expand(X, Y, w, logh, B, tabs, L1, L2, st));
+    LSP_HIP(launch_ntt(Y, (size_t)B * w, logh, ctx->twiddle(logh, false), true, st));
+    // out block k = transpose of Y_k (w x h) -> h x w
+    LSP_HIP(launch_transpose(Y, d_out, B, w, h, false, st));
+    // host vectors (bases, scales) must outlive the async copies
+    LSP_HIP(hipStreamSynchronize(st));
+}
+
+// ------------------------------------------------------------- Merkle
+Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers) {
+    LSP_HIP(launch_hash_rows(m, height, layers, ctx->rc_dev, ctx->p2.L, ctx->stream));
+    LSP_HIP(launch_merkle_tree(layers, height, ctx->rc_dev, ctx->p2.L, ctx->stream));
+    return d2h_fr(ctx, layers + 2 * height - 2);
+}
+
+static MatList one_mat(const Fr* p, uint32_t w) {
+    MatList m{};
+    m.ptr[0] = p;
+    m.width[0] = w;
+    m.n = 1;
+    return m;
+}
+
+static void tree_path(const std::vector<Fr>& got, size_t& cur, uint32_t lg, std::vector<Fr>& out) {
+    out.assign(got.begin() + cur, got.begin() + cur + lg);
+    cur += lg;
+}
+
+// ------------------------------------------------------------- prove
+lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, const Air& air, const Fr* pub,
+                        size_t npub) {
+    LSP_REQUIRE(npub >= 2, LSP_E_ARG, "public values must hold [alpha, delta]");
+    LSP_REQUIRE(air.max_col < w, LSP_E_ARG, "AIR column id outside the trace width");
+    const uint32_t log_h = log2_exact(h);
+    LSP_REQUIRE(h >= 2, LSP_E_SIZE, "trace needs at least 2 rows");
+    const uint32_t lb = ctx->log_blowup;
+    const uint32_t log_q = air.log_quotient_degree(ctx->public_degree);
+    LSP_REQUIRE(log_q <= lb, LSP_E_ARG, "quotient degree exceeds the blowup");
+    const size_t q = (size_t)1 << log_q;
+    const uint32_t logN = log_h + lb, logQ = log_h + log_q;
+    const size_t N = (size_t)1 << logN, Q = (size_t)1 << logQ;
+    LSP_REQUIRE(logN <= 40, LSP_E_SIZE, "trace too large");
+    hipStream_t st = ctx->stream;
+    const Fr GEN = host_generator();
+    const Fr one = fr_one();
+    PhaseTimer T(ctx);
+    auto* proof = new lsp_proof();
+    proof->log_h = log_h;
+    proof->log_q = log_q;
+    proof->w = (uint32_t)w;
+    try {
+        T.begin("prove");
+        // ---- commit to trace data
+        T.begin("commit to trace data");
+        Fr* lde = ctx->fbuf("t_lde", N * w);
+        std::vector<Fr> shifts(std::max(w, q), GEN);
+        T.begin("coset_lde_batch");
+        lde_device(ctx, d_trace, h, w, lb, shifts.data(), lde);
+        T.end("coset_lde_batch");
+        Fr* tlay = ctx->fbuf("t_tree", 2 * N - 1);
+        T.begin("merkle tree");
+        proof->troot = commit_device(ctx, one_mat(lde, (uint32_t)w), N, tlay);
+        T.end("merkle tree");
+        T.end("commit to trace data");
+
+        Challenger ch(&ctx->p2);
+        ch.observe(fr_from_u64(log_h));
+        ch.observe(proof->troot);
+        for (size_t i = 0; i < npub; ++i) ch.observe(pub[i]);
+        const Fr alpha = ch.sample();
+
+        // ---- quotient
+        T.begin("compute quotient polynomial");
+        uint32_t L1Q;
+        const Fr* tabQ = pow_table(ctx, "tabQ", host_two_adic_generator(logQ), logQ, L1Q);
+        const Fr wh = host_two_adic_generator(log_h);
+        const Fr wh_inv = fr_inv(wh);
+        Fr* den = ctx->fbuf("q_den", Q);
+        Fr* inv_den = ctx->fbuf("q_invden", Q);
+        LSP_HIP(launch_selector_denoms(tabQ, L1Q, GEN, wh_inv, Q, den, st));
+        LSP_HIP(launch_batch_inverse(den, inv_den, Q, st));
+        std::vector<Fr> zh(q), izh(q);
+        {
+            const Fr gh = fr_pow_u64(GEN, h), gq = host_two_adic_generator(log_q);
+            Fr g = one;
+            for (size_t k = 0; k < q; ++k) {
+                zh[k] = fr_sub(fr_mul(gh, g), one);
+                izh[k] = fr_inv(zh[k]);
+                g = fr_mul(g, gq);
+            }
+        }
+        Fr* dzh = ctx->fbuf("q_zh", 2 * q);
+        LSP_HIP(hipMemcpyAsync(dzh, zh.data(), q * sizeof(Fr), hipMemcpyHostToDevice, st));
+        LSP_HIP(hipMemcpyAsync(dzh + q, izh.data(), q * sizeof(Fr), hipMemcpyHostToDevice, st));
+        int32_t* dair = (int32_t*)ctx->buf("air", air.raw.size() * sizeof(int32_t));
+        LSP_HIP(hipMemcpyAsync(dair, air.raw.data(), air.raw.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        Fr* qv = ctx->fbuf("q_values", Q);
+        QuotientArgs qa;
+        qa.lde = lde;
+        qa.w = (uint32_t)w;
+        qa.logQ = logQ;
+        qa.log_q = log_q;
+        qa.air = dair;
+        qa.air_len = (uint32_t)air.raw.size();
+        qa.pub_alpha = pub[0];
+        qa.pub_delta = pub[1];
+        qa.alpha = alpha;
+        qa.gen = GEN;
+        qa.wh_inv = wh_inv;
+        qa.tabQ = tabQ;
+        qa.L1 = L1Q;
+        qa.zh = dzh;
+        qa.inv_zh = dzh + q;
+        qa.inv_den = inv_den;
+        qa.out = qv;
+        LSP_HIP(launch_quotient(qa, st));
+        T.end("compute quotient polynomial");
+
+        // ---- commit to quotient chunks: qv is the h x q matrix of chunks
+        T.begin("commit to quotient poly chunks");
+        const Fr gQ = host_two_adic_generator(logQ), gQinv = fr_inv(gQ);
+        {
+            Fr s = one;
+            for (size_t j = 0; j < q; ++j) {
+                shifts[j] = s;  // GEN / (GEN * w_Q^j)
+                s = fr_mul(s, gQinv);
+            }
+        }
+        Fr* qlde = ctx->fbuf("q_lde", N * q);
+        T.begin("coset_lde_batch (quotient)");
+        lde_device(ctx, qv, h, q, lb, shifts.data(), qlde);
+        T.end("coset_lde_batch (quotient)");
+        Fr* qlay = ctx->fbuf("q_tree", 2 * N - 1);
+        proof->qroot = commit_device(ctx, one_mat(qlde, (uint32_t)q), N, qlay);
+        T.end("commit to quotient poly chunks");
+        ch.observe(proof->qroot);
+        const Fr zeta = ch.sample();
+        const Fr zeta_next = fr_mul(zeta, wh);
+
+        // ---- open
+        T.begin("open");
+        const Fr alpha_fri = ch.sample();
+        T.begin("compute_inverse_denominators");
+        uint32_t L1N;
+        const Fr* tabN = pow_table(ctx, "tabN", host_two_adic_generator(logN), logN, L1N);
+        Fr* dtmp = ctx->fbuf("o_den", N);
+        Fr* inv_z = ctx->fbuf("o_invz", N);
+        Fr* inv_zn = ctx->fbuf("o_invzn", N);
+        LSP_HIP(launch_open_denoms(zeta, GEN, tabN, L1N, logN, N, dtmp, st));
+        LSP_HIP(launch_batch_inverse(dtmp, inv_z, N, st));
+        LSP_HIP(launch_open_denoms(zeta_next, GEN, tabN, L1N, logN, N, dtmp, st));
+        LSP_HIP(launch_batch_inverse(dtmp, inv_zn, N, st));
+        T.end("compute_inverse_denominators");
+        T.begin("compute opened values with Lagrange interpolation");
+        // barycentric sums on the low coset (first h rows), then the host-side factor
+        const size_t maxw = std::max(w, q);
+        Fr* partial = ctx->fbuf("o_partial", ((h + 1023) / 1024) * maxw);
+        Fr* sums = ctx->fbuf("o_sums", 2 * w + q);
+        uint32_t nb = 0;
+        LSP_HIP(launch_interp_partial(lde, (uint32_t)w, h, inv_z, GEN, tabN, L1N, logN, partial, &nb, st));
+        LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)w, sums, st));
+        LSP_HIP(launch_interp_partial(lde, (uint32_t)w, h, inv_zn, GEN, tabN, L1N, logN, partial, &nb, st));
+        LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)w, sums + w, st));
+        LSP_HIP(launch_interp_partial(qlde, (uint32_t)q, h, inv_z, GEN, tabN, L1N, logN, partial, &nb, st));
+        LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)q, sums + 2 * w, st));
+        std::vector<Fr> hs(2 * w + q);
+        LSP_HIP(hipMemcpyAsync(hs.data(), sums, hs.size() * sizeof(Fr), hipMemcpyDeviceToHost, st));
+        LSP_HIP(hipStreamSynchronize(st));
+        const Fr gh = fr_pow_u64(GEN, h);
+        const Fr dinv = fr_inv(fr_mul(gh, fr_from_u64(h)));
+        auto factor = [&](const Fr& z) { return fr_mul(fr_sub(fr_pow_u64(z, h), gh), dinv); };
+        const Fr fz = factor(zeta), fzn = factor(zeta_next);
+        proof->tl.resize(w);
+        proof->tn.resize(w);
+        proof->qc.resize(q);
+        for (size_t c = 0; c < w; ++c) {
+            proof->tl[c] = fr_mul(hs[c], fz);
+            proof->tn[c] = fr_mul(hs[w + c], fzn);
+        }
+        for (size_t j = 0; j < q; ++j) proof->qc[j] = fr_mul(hs[2 * w + j], fz);
+        T.end("compute opened values with Lagrange interpolation");
+
+        T.begin("reduce rows");
+        std::vector<Fr> apw(2 * w + q);
+        apw[0] = one;
+        for (size_t k = 1; k < apw.size(); ++k) apw[k] = fr_mul(apw[k - 1], alpha_fri);
+        Fr ry_z = fr_zero(), ry_zn = fr_zero();
+        for (size_t c = 0; c < w; ++c) {
+            ry_z = fr_add(ry_z, fr_mul(apw[c], proof->tl[c]));
+            ry_zn = fr_add(ry_zn, fr_mul(apw[c], proof->tn[c]));
+        }
+        Fr* dapw = ctx->fbuf("o_apw", apw.size() + q);
+        LSP_HIP(hipMemcpyAsync(dapw, apw.data(), apw.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
+        LSP_HIP(hipMemcpyAsync(dapw + apw.size(), proof->qc.data(), q * sizeof(Fr), hipMemcpyHostToDevice, st));
+        // FRI vectors: round r input of length N >> r, stored back to back
+        Fr* fvec = ctx->fbuf("f_vec", 2 * N);
+        ReduceArgs ra;
+        ra.lde = lde;
+        ra.w = (uint32_t)w;
+        ra.qlde = qlde;
+        ra.q = (uint32_t)q;
+        ra.inv_z = inv_z;
+        ra.inv_zn = inv_zn;
+        ra.apw = dapw;
+        ra.ry_z = ry_z;
+        ra.ry_zn = ry_zn;
+        ra.ryq = dapw + apw.size();
+        ra.out = fvec;
+        ra.n = N;
+        LSP_HIP(launch_reduce_rows(ra, st));
+        LSP_HIP(hipStreamSynchronize(st));  // apw/qc host vectors
+        T.end("reduce rows");
+
+        // ---- FRI commit phase
+        T.begin("FRI prover");
+        T.begin("commit phase");
+        const size_t final_len = (size_t)1 << (lb + ctx->log_final_poly_len);
+        std::vector<size_t> voff, toff;
+        Fr* ftree = ctx->fbuf("f_tree", 2 * N);
+        size_t len = N, vo = 0, to = 0;
+        const Fr half = fr_inv(fr_from_u64(2));
+        while (len > final_len) {
+            const size_t m = len / 2;
+            voff.push_back(vo);
+            toff.push_back(to);
+            const Fr root = commit_device(ctx, one_mat(fvec + vo, 2), m, ftree + to);
+            proof->roots.push_back(root);
+            ch.observe(root);
+            const Fr beta = ch.sample();
+            uint32_t L1F;
+            const uint32_t logm = log2_exact(m);
+            const Fr ginv = fr_inv(host_two_adic_generator(logm + 1));
+            const Fr* tabF = pow_table(ctx, "tabF", ginv, logm, L1F);
+            LSP_HIP(launch_fri_fold(fvec + vo, m, half, fr_mul(beta, half), tabF, L1F, fvec + vo + len, st));
+            vo += len;
+            to += 2 * m - 1;
+            len = m;
+        }
+        std::vector<Fr> fin(len);
+        LSP_HIP(hipMemcpyAsync(fin.data(), fvec + vo, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
+        LSP_HIP(hipStreamSynchronize(st));
+        T.end("commit phase");
+        {
+            // final poly: bit-reverse, IDFT (naive, len <= 2^lb small), truncate
+            const uint32_t lgl = log2_exact(len);
+            std::vector<Fr> br(len);
+            for (size_t i = 0; i < len; ++i) br[i] = fin[host_bitrev(i, lgl)];
+            const Fr winv = fr_inv(host_two_adic_generator(lgl));
+            const Fr linv = fr_inv(fr_from_u64(len));
+            const size_t flen = (size_t)1 << ctx->log_final_poly_len;
+            for (size_t k = 0; k < len; ++k) {
+                Fr acc = fr_zero();
+                const Fr wk = fr_pow_u64(winv, k);
+                Fr p = one;
+                for (size_t j = 0; j < len; ++j) {
+                    acc = fr_add(acc, fr_mul(br[j], p));
+                    p = fr_mul(p, wk);
+                }
+                acc = fr_mul(acc, linv);
+                if (k < flen)
+                    proof->final_poly.push_back(acc);
+                else
+                    LSP_REQUIRE(fr_is_zero(acc), LSP_E_STATE, "FRI final polynomial degree too high");
+            }
+            for (const Fr& c : proof->final_poly) ch.observe(c);
+        }
+        T.begin("grind for proof-of-work witness");
+        proof->pow_w = fr_from_u64(ch.grind(ctx->pow_bits));
+        T.end("grind for proof-of-work witness");
+
+        // ---- query phase: one gather for every opened element
+        T.begin("query phase");
+        const uint32_t nr = (uint32_t)proof->roots.size();
+        std::vector<uint64_t> ptrs;
+        std::vector<size_t> idxs(ctx->num_queries);
+        for (uint32_t qi = 0; qi < ctx->num_queries; ++qi) {
+            const size_t idx = (size_t)ch.sample_bits(logN);
+            idxs[qi] = idx;
+            auto P = [&](const Fr* p) { ptrs.push_back((uint64_t)(uintptr_t)p); };
+            for (size_t c = 0; c < w; ++c) P(lde + idx * w + c);
+            {
+                size_t off = 0, ln = N;
+                for (uint32_t i = 0; i < logN; ++i) {
+                    P(tlay + off + ((idx >> i) ^ 1));
+                    off += ln;
+                    ln >>= 1;
+                }
+            }
+            for (size_t j = 0; j < q; ++j) P(qlde + idx * q + j);
+            {
+                size_t off = 0, ln = N;
+                for (uint32_t i = 0; i < logN; ++i) {
+                    P(qlay + off + ((idx >> i) ^ 1));
+                    off += ln;
+                    ln >>= 1;
+                }
+            }
+            size_t l2 = N;
+            for (uint32_t r = 0; r < nr; ++r) {
+                const size_t m = l2 / 2, ii = idx >> r, pair = ii >> 1;
+                P(fvec + voff[r] + (ii ^ 1));
+                size_t off = toff[r], ln = m;
+                const uint32_t lg = log2_exact(m);
+                for (uint32_t i = 0; i < lg; ++i) {
+                    P(ftree + off + ((pair >> i) ^ 1));
+                    off += ln;
+                    ln >>= 1;
+                }
+                l2 = m;
+            }
+        }
+        uint64_t* dptrs = (uint64_t*)ctx->buf("g_ptrs", ptrs.size() * sizeof(uint64_t));
+        Fr* dgot = ctx->fbuf("g_out", ptrs.size());
+        LSP_HIP(hipMemcpyAsync(dptrs, ptrs.data(), ptrs.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+        LSP_HIP(launch_gather(dptrs, dgot, ptrs.size(), st));
+        std::vector<Fr> got(ptrs.size());
+        LSP_HIP(hipMemcpyAsync(got.data(), dgot, got.size() * sizeof(Fr), hipMemcpyDeviceToHost, st));
+        LSP_HIP(hipStreamSynchronize(st));
+        size_t cur = 0;
+        for (uint32_t qi = 0; qi < ctx->num_queries; ++qi) {
+            lsp_query qq;
+            qq.trow.assign(got.begin() + cur, got.begin() + cur + w);
+            cur += w;
+            tree_path(got, cur, logN, qq.tpath);
+            qq.qrow.assign(got.begin() + cur, got.begin() + cur + q);
+            cur += q;
+            tree_path(got, cur, logN, qq.qpath);
+            for (uint32_t r = 0; r < nr; ++r) {
+                qq.sib.push_back(got[cur++]);
+                std::vector<Fr> pth;
+                tree_path(got, cur, logN - r - 1, pth);
+                qq.fpath.push_back(std::move(pth));
+            }
+            proof->queries.push_back(std::move(qq));
+        }
+        T.end("query phase");
+        T.end("FRI prover");
+        T.end("open");
+        T.end("prove");
+        T.collect();
+    } catch (...) {
+        delete proof;
+        throw;
+    }
+    return proof;
+}
+
+// --------------------------------------------------------- serialization
+static void put_u32(std::vector<uint8_t>& b, uint32_t x) {
+    for (int i = 0; i < 4; ++i) b.push_back((uint8_t)(x >> (8 * i)));
+}
+static void put_fr(std::vector<uint8_t>& b, const Fr& x) {
+    const Fr c = fr_to_canonical(x);
+    for (int i = 0; i < 8; ++i) put_u32(b, c.v[i]);
+}
+
+std::vector<uint8_t> serialize(const lsp_proof& p) {
+    std::vector<uint8_t> b;
+    const char* magic = "LSPPRF01";
+    b.insert(b.end(), magic, magic + 8);
+    put_u32(b, p.log_h);
+    put_u32(b, p.log_q);
+    put_u32(b, p.w);
+    put_u32(b, (uint32_t)p.queries.size());
+    put_u32(b, (uint32_t)p.roots.size());
+    put_fr(b, p.troot);
+    put_fr(b, p.qroot);
+    for (auto& x : p.tl) put_fr(b, x);
+    for (auto& x : p.tn) put_fr(b, x);
+    for (auto& x : p.qc) put_fr(b, x);
+    for (auto& x : p.roots) put_fr(b, x);
+    for (auto& x : p.final_poly) put_fr(b, x);
+    put_fr(b, p.pow_w);
+    for (auto& q : p.queries) {
+        for (auto& x : q.trow) put_fr(b, x);
+        put_u32(b, (uint32_t)q.tpath.size());
+        for (auto& x : q.tpath) put_fr(b, x);
+        for (auto& x : q.qrow) put_fr(b, x);
+        put_u32(b, (uint32_t)q.qpath.size());
+        for (auto& x : q.qpath) put_fr(b, x);
+        for (size_t r = 0; r < q.sib.size(); ++r) {
+            put_fr(b, q.sib[r]);
+            put_u32(b, (uint32_t)q.fpath[r].size());
+            for (auto& x : q.fpath[r]) put_fr(b, x);
+        }
+    }
+    return b;
+}
+
+}  // namespace lsp

@@ -1,0 +1,335 @@
+"""Python mirror of the reference's plug point (bin/src/config.rs:9-25) over
+the C-ABI of liblsp_hip.so.
+
+Reference item                                   -> here
+  StarkConfig / FriConfig / Perm::new_from_rng    -> StarkConfig (+ seeded U4/U5 setup)
+  Radix2DitParallel::coset_lde_batch (Dft)        -> Radix2DitParallel.coset_lde_batch
+  MerkleTreeMmcs commit/open_batch/verify_batch   -> MerkleTreeMmcs
+  TwoAdicFriGenericConfig::fold_matrix/fold_row   -> TwoAdicFriGenericConfig
+  p3_uni_stark::quotient_values                   -> Context.quotient_values
+  p3_interpolation::interpolate_coset             -> Context.interpolate_coset
+  p3_uni_stark::prove / verify (main.rs:80-96)    -> prove / verify
+
+Arrays are numpy uint64 with a trailing axis of 4 limbs (Montgomery form).
+Everything runs through the HIP library; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+from .air import LineaAIR
+from .field import to_mont
+
+DEFAULT_SEED = 0x4C494E4541  # "LINEA"
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def _fr_arr(a) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.uint64)
+    assert a.shape[-1] == 4, "element arrays need a trailing axis of 4 limbs"
+    return a
+
+
+@dataclass
+class StarkConfig:
+    """bin/src/config.rs:9-25 + bin/src/main.rs:49-64 (+ the U1/U6 switches)."""
+    sbox_degree: int = 11           # U1
+    rounds_f: int = 8               # Perm::new_from_rng(8, 22)
+    rounds_p: int = 22
+    log_blowup: int = 3             # FriConfig
+    log_final_poly_len: int = 0
+    num_queries: int = 33
+    proof_of_work_bits: int = 0
+    public_degree: int = 1          # U6
+    seed: int = DEFAULT_SEED        # U4/U5
+
+    def seeded(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(alpha, delta, round_constants) from the documented seeded generator."""
+        n = 3 * self.rounds_f + self.rounds_p
+        a, d, rc = np.zeros((1, 4), np.uint64), np.zeros((1, 4), np.uint64), np.zeros((n, 4), np.uint64)
+        L.check(L.lib().lsp_seeded_setup(self.seed, self.rounds_f, self.rounds_p, _ptr(a), _ptr(d), _ptr(rc)))
+        return a, d, rc
+
+
+class Context:
+    """One lsp_ctx: a GPU, a stream, the Poseidon2 constants and a buffer pool."""
+
+    def __init__(self, config: StarkConfig = StarkConfig(), device: int = 0,
+                 round_constants: Optional[np.ndarray] = None):
+        self.config = config
+        if round_constants is None:
+            _, _, round_constants = config.seeded()
+        self._rc = _fr_arr(round_constants)
+        p = L.LspParams(config.sbox_degree, config.rounds_f, config.rounds_p, _ptr(self._rc), config.log_blowup,
+                        config.log_final_poly_len, config.num_queries, config.proof_of_work_bits,
+                        config.public_degree)
+        h = ctypes.c_void_p()
+        L.check(L.lib().lsp_ctx_create(device, ctypes.byref(p), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            L.lib().lsp_ctx_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        L.check(rc, self.h)
+
+    def synchronize(self):
+        self._chk(L.lib().lsp_synchronize(self.h))
+
+    # ---------------------------------------------------------- device buffers
+    def dev_alloc(self, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        self._chk(L.lib().lsp_dev_alloc(self.h, nbytes, ctypes.byref(p)))
+        return p.value
+
+    def dev_free(self, p: int):
+        self._chk(L.lib().lsp_dev_free(self.h, p))
+
+    def h2d(self, dst: int, a: np.ndarray):
+        a = np.ascontiguousarray(a)
+        self._chk(L.lib().lsp_memcpy_h2d(self.h, dst, _ptr(a), a.nbytes))
+
+    def d2h(self, a: np.ndarray, src: int):
+        self._chk(L.lib().lsp_memcpy_d2h(self.h, _ptr(a), src, a.nbytes))
+
+    # ------------------------------------------------------------------- Dft
+    def coset_lde_batch(self, mat: np.ndarray, added_bits: int, shift) -> np.ndarray:
+        mat = _fr_arr(mat)
+        h, w = mat.shape[0], mat.shape[1]
+        out = np.zeros((h << added_bits, w, 4), np.uint64)
+        sh = _fr_arr(shift).reshape(-1, 4)
+        if sh.shape[0] == 1:
+            self._chk(L.lib().lsp_coset_lde_batch(self.h, _ptr(mat), h, w, added_bits, _ptr(sh), _ptr(out),
+                                                  L.LSP_MEM_HOST))
+        else:
+            assert sh.shape[0] == w
+            self._chk(L.lib().lsp_coset_lde_batch_shifts(self.h, _ptr(mat), h, w, added_bits, _ptr(sh), _ptr(out),
+                                                         L.LSP_MEM_HOST))
+        return out
+
+    # -------------------------------------------------------------- symmetric
+    def poseidon2_permute(self, states: np.ndarray) -> np.ndarray:
+        s = _fr_arr(states).copy()
+        self._chk(L.lib().lsp_poseidon2_permute_batch(self.h, _ptr(s), s.shape[0], L.LSP_MEM_HOST))
+        return s
+
+    def hash_rows(self, rows: np.ndarray) -> np.ndarray:
+        rows = _fr_arr(rows)
+        out = np.zeros((rows.shape[0], 4), np.uint64)
+        self._chk(L.lib().lsp_hash_rows(self.h, _ptr(rows), rows.shape[0], rows.shape[1], _ptr(out),
+                                        L.LSP_MEM_HOST))
+        return out
+
+    # -------------------------------------------------------------- quotient
+    def quotient_values(self, lde: np.ndarray, h: int, air: LineaAIR, public_values: np.ndarray,
+                        alpha: np.ndarray) -> np.ndarray:
+        lde = _fr_arr(lde)
+        desc = (ctypes.c_int32 * len(air.descriptor()))(*air.descriptor())
+        lq = ctypes.c_uint32()
+        L.check(L.lib().lsp_log_quotient_degree(desc, len(desc), self.config.public_degree, ctypes.byref(lq)))
+        out = np.zeros((h << lq.value, 4), np.uint64)
+        pub = _fr_arr(public_values).reshape(-1, 4)
+        al = _fr_arr(alpha).reshape(-1, 4)
+        self._chk(L.lib().lsp_quotient_values(self.h, _ptr(lde), h, lde.shape[1], desc, len(desc), _ptr(pub),
+                                              pub.shape[0], _ptr(al), _ptr(out), L.LSP_MEM_HOST))
+        return out
+
+    def interpolate_coset(self, lde_bitrev: np.ndarray, h: int, shift, z) -> np.ndarray:
+        m = _fr_arr(lde_bitrev)
+        w = m.shape[1]
+        out = np.zeros((w, 4), np.uint64)
+        sh, zz = _fr_arr(shift).reshape(-1, 4), _fr_arr(z).reshape(-1, 4)
+        self._chk(L.lib().lsp_interpolate_coset(self.h, _ptr(m), h, w, _ptr(sh), _ptr(zz), _ptr(out),
+                                                L.LSP_MEM_HOST))
+        return out
+
+    def batch_inverse(self, x: np.ndarray) -> np.ndarray:
+        x = _fr_arr(x).reshape(-1, 4)
+        out = np.zeros_like(x)
+        self._chk(L.lib().lsp_batch_inverse(self.h, _ptr(x), x.shape[0], _ptr(out), L.LSP_MEM_HOST))
+        return out
+
+    # ----------------------------------------------------------------- prove
+    def prove(self, trace, air: LineaAIR, public_values: np.ndarray, h: Optional[int] = None,
+              w: Optional[int] = None) -> bytes:
+        """p3_uni_stark::prove.  `trace` is an (h, w, 4) host array, or a device
+        pointer (int) to an h x w matrix with h and w given."""
+        desc = (ctypes.c_int32 * len(air.descriptor()))(*air.descriptor())
+        pub = _fr_arr(public_values).reshape(-1, 4)
+        proof = ctypes.c_void_p()
+        if isinstance(trace, int):
+            self._chk(L.lib().lsp_prove(self.h, trace, h, w, desc, len(desc), _ptr(pub), pub.shape[0],
+                                        L.LSP_MEM_DEVICE, ctypes.byref(proof)))
+        else:
+            t = _fr_arr(trace)
+            self._chk(L.lib().lsp_prove(self.h, _ptr(t), t.shape[0], t.shape[1], desc, len(desc), _ptr(pub),
+                                        pub.shape[0], L.LSP_MEM_HOST, ctypes.byref(proof)))
+        try:
+            n = ctypes.c_size_t()
+            L.check(L.lib().lsp_proof_serialize(proof, None, 0, ctypes.byref(n)))
+            buf = ctypes.create_string_buffer(n.value)
+            L.check(L.lib().lsp_proof_serialize(proof, buf, n.value, ctypes.byref(n)))
+            return buf.raw[:n.value]
+        finally:
+            L.lib().lsp_proof_free(proof)
+
+    def verify(self, proof: bytes, air: LineaAIR, public_values: np.ndarray) -> bool:
+        desc = (ctypes.c_int32 * len(air.descriptor()))(*air.descriptor())
+        pub = _fr_arr(public_values).reshape(-1, 4)
+        rc = L.lib().lsp_verify(self.h, desc, len(desc), _ptr(pub), pub.shape[0], proof, len(proof))
+        if rc == L.LSP_E_VERIFY:
+            return False
+        L.check(rc)
+        return True
+
+    def last_timings(self) -> List[Tuple[str, float]]:
+        n = ctypes.c_size_t()
+        L.lib().lsp_last_timings(self.h, None, None, 0, ctypes.byref(n))
+        ms = (ctypes.c_double * n.value)()
+        names = (ctypes.c_char_p * n.value)()
+        L.lib().lsp_last_timings(self.h, ms, names, n.value, ctypes.byref(n))
+        return [(names[i].decode(), ms[i]) for i in range(n.value)]
+
+
+class Radix2DitParallel:
+    """TwoAdicSubgroupDft (bin/src/config.rs:22) on the GPU; returns the
+    bit-reversed rows TwoAdicFriPcs::commit consumes."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def coset_lde_batch(self, mat: np.ndarray, added_bits: int, shift) -> np.ndarray:
+        return self.ctx.coset_lde_batch(mat, added_bits, shift)
+
+
+class MerkleTree:
+    def __init__(self, ctx: Context, handle, height: int, widths: Sequence[int]):
+        self.ctx, self.handle, self.height, self.widths = ctx, handle, height, list(widths)
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            L.lib().lsp_tree_free(self.handle)
+            self.handle = None
+
+    def layer(self, level: int) -> np.ndarray:
+        out = np.zeros((self.height >> level, 4), np.uint64)
+        self.ctx._chk(L.lib().lsp_merkle_layer(self.handle, level, _ptr(out)))
+        return out
+
+
+class MerkleTreeMmcs:
+    """MerkleTreeMmcs<Val, Val, Hash, Compress, 1> (bin/src/config.rs:19-20)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def commit(self, mats: Sequence[np.ndarray]) -> Tuple[np.ndarray, MerkleTree]:
+        mats = [_fr_arr(m) for m in mats]
+        hgt = mats[0].shape[0]
+        assert all(m.shape[0] == hgt for m in mats), "equal heights only"
+        ptrs = (ctypes.c_void_p * len(mats))(*[_ptr(m) for m in mats])
+        widths = (ctypes.c_size_t * len(mats))(*[m.shape[1] for m in mats])
+        root = np.zeros((1, 4), np.uint64)
+        t = ctypes.c_void_p()
+        self.ctx._chk(L.lib().lsp_merkle_commit(self.ctx.h, ptrs, widths, len(mats), hgt, L.LSP_MEM_HOST,
+                                                _ptr(root), ctypes.byref(t)))
+        return root, MerkleTree(self.ctx, t, hgt, [m.shape[1] for m in mats])
+
+    def open_batch(self, index: int, tree: MerkleTree) -> Tuple[List[np.ndarray], np.ndarray]:
+        rows = np.zeros((sum(tree.widths), 4), np.uint64)
+        path = np.zeros((max(tree.height.bit_length() - 1, 1), 4), np.uint64)
+        self.ctx._chk(L.lib().lsp_merkle_open(tree.handle, index, _ptr(rows), _ptr(path)))
+        out, o = [], 0
+        for w in tree.widths:
+            out.append(rows[o:o + w])
+            o += w
+        return out, path[:tree.height.bit_length() - 1]
+
+    def verify_batch(self, root: np.ndarray, widths: Sequence[int], log_height: int, index: int,
+                     rows: Sequence[np.ndarray], path: np.ndarray) -> bool:
+        flat = _fr_arr(np.concatenate([_fr_arr(r).reshape(-1, 4) for r in rows]))
+        ws = (ctypes.c_size_t * len(widths))(*widths)
+        p = _fr_arr(path).reshape(-1, 4) if log_height else np.zeros((1, 4), np.uint64)
+        rc = L.lib().lsp_merkle_verify(self.ctx.h, _ptr(_fr_arr(root)), ws, len(widths), log_height, index,
+                                       _ptr(flat), _ptr(p))
+        return rc == L.LSP_OK
+
+
+class TwoAdicFriGenericConfig:
+    """The north_star's 'FriFolder' ([EXT p3-fri] FriGenericConfig)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def fold_matrix(self, beta: np.ndarray, v: np.ndarray) -> np.ndarray:
+        v = _fr_arr(v).reshape(-1, 4)
+        out = np.zeros((v.shape[0] // 2, 4), np.uint64)
+        b = _fr_arr(beta).reshape(-1, 4)
+        self.ctx._chk(L.lib().lsp_fri_fold(self.ctx.h, _ptr(v), v.shape[0], _ptr(b), _ptr(out), L.LSP_MEM_HOST))
+        return out
+
+    @staticmethod
+    def fold_row(index: int, log_height: int, beta: np.ndarray, e0: np.ndarray, e1: np.ndarray) -> np.ndarray:
+        out = np.zeros((1, 4), np.uint64)
+        L.lib().lsp_fri_fold_row(index, log_height, _ptr(_fr_arr(beta)), _ptr(_fr_arr(e0)), _ptr(_fr_arr(e1)),
+                                 _ptr(out))
+        return out
+
+
+def gen_permutation_trace(log_n: int, ncols: int, alpha: np.ndarray, delta: np.ndarray,
+                          seed: int = DEFAULT_SEED, small_values: bool = False) -> np.ndarray:
+    """Synthetic trace of SURVEY 8(d) C1 with RawPermutationTrace's witness
+    columns (trace/src/permutation.rs:24-93): (2^log_n, 2*ncols+2, 4)."""
+    out = np.zeros((1 << log_n, 2 * ncols + 2, 4), np.uint64)
+    L.check(L.lib().lsp_gen_permutation_trace(seed, log_n, ncols, _ptr(_fr_arr(alpha)), _ptr(_fr_arr(delta)),
+                                              int(small_values), _ptr(out)))
+    return out
+
+
+def prove(config: StarkConfig, air: LineaAIR, trace: np.ndarray, public_values: np.ndarray,
+          ctx: Optional[Context] = None) -> bytes:
+    """p3_uni_stark::prove(&config, &air, &mut challenger, trace, &public_values)."""
+    own = ctx is None
+    ctx = ctx or Context(config)
+    try:
+        return ctx.prove(trace, air, public_values)
+    finally:
+        if own:
+            ctx.close()
+
+
+def verify(config: StarkConfig, air: LineaAIR, proof: bytes, public_values: np.ndarray,
+           ctx: Optional[Context] = None) -> bool:
+    own = ctx is None
+    ctx = ctx or Context(config)
+    try:
+        return ctx.verify(proof, air, public_values)
+    finally:
+        if own:
+            ctx.close()
+
+
+__all__ = ["StarkConfig", "Context", "Radix2DitParallel", "MerkleTreeMmcs", "MerkleTree",
+           "TwoAdicFriGenericConfig", "gen_permutation_trace", "prove", "verify", "to_mont"]

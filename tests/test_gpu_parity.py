@@ -1,0 +1,295 @@
+"""GPU parity: every hot-path stage of liblsp_hip.so against the oracle.
+
+Checker: oracle/lsp_oracle.c (C restatement, pinned to oracle/pyoracle.py by
+tests/test_oracle.py) and, at tiny sizes, pyoracle itself.  Everything here is
+integer arithmetic mod r, so the bar is bit-exact equality.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+P = O.P
+
+
+def rand_fr(rng, shape):
+    """uniform canonical Fr in Montgomery limbs"""
+    n = int(np.prod(shape))
+    vals = [int.from_bytes(rng.bytes(32), "little") % P for _ in range(n)]
+    from linea_stark_prover_amd.field import to_mont
+    return to_mont(vals).reshape(tuple(shape) + (4,))
+
+
+def ints(a):
+    from linea_stark_prover_amd.field import from_mont
+    return from_mont(a)
+
+
+def oracle_params(oracle_lib):
+    return oracle_lib.setup()
+
+
+def c_ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+# ------------------------------------------------------------------ LDE
+@pytest.mark.parametrize("logh,w,added", [(1, 1, 1), (3, 2, 3), (5, 8, 3), (8, 14, 3), (10, 4, 2), (12, 8, 3),
+                                          (13, 3, 3), (11, 1, 3)])
+def test_coset_lde_matches_oracle(gpu_ctx, oracle_lib, logh, w, added):
+    rng = np.random.default_rng(logh * 100 + w)
+    h = 1 << logh
+    mat = rand_fr(rng, (h, w))
+    shift = rand_fr(rng, (1,))
+    got = gpu_ctx.coset_lde_batch(mat, added, shift)
+    exp = np.zeros_like(got)
+    shifts = np.repeat(shift.reshape(1, 4), w, axis=0).copy()
+    oracle_lib.lib().lo_coset_lde_batch(c_ptr(mat), ctypes.c_size_t(h), ctypes.c_size_t(w), added, c_ptr(shifts),
+                                        c_ptr(exp), 8)
+    assert np.array_equal(got, exp)
+
+
+def test_coset_lde_per_column_shifts(gpu_ctx, oracle_lib):
+    rng = np.random.default_rng(7)
+    h, w, added = 1 << 9, 4, 3
+    mat = rand_fr(rng, (h, w))
+    shifts = rand_fr(rng, (w,))
+    got = gpu_ctx.coset_lde_batch(mat, added, shifts)
+    exp = np.zeros_like(got)
+    oracle_lib.lib().lo_coset_lde_batch(c_ptr(mat), ctypes.c_size_t(h), ctypes.c_size_t(w), added, c_ptr(shifts),
+                                        c_ptr(exp), 8)
+    assert np.array_equal(got, exp)
+
+
+def test_coset_lde_tiny_vs_pyoracle(gpu_ctx):
+    rng = np.random.default_rng(3)
+    h, w = 8, 3
+    mat = rand_fr(rng, (h, w))
+    rows = [ints(mat[i]) for i in range(h)]
+    exp = O.coset_lde_batch(rows, 3, O.GENERATOR)
+    from linea_stark_prover_amd.field import to_mont
+    got = gpu_ctx.coset_lde_batch(mat, 3, to_mont([O.GENERATOR]))
+    assert [ints(got[i]) for i in range(len(exp))] == exp
+
+
+# ------------------------------------------------------------- Poseidon2
+def test_poseidon2_permute_matches_oracle(gpu_ctx, oracle_lib):
+    rng = np.random.default_rng(11)
+    n = 4099
+    st = rand_fr(rng, (n, 3))
+    got = gpu_ctx.poseidon2_permute(st)
+    p = oracle_params(oracle_lib)
+    exp = st.copy()
+    for i in range(n):
+        oracle_lib.lib().lo_poseidon2_permute(ctypes.byref(p), c_ptr(exp[i]))
+    assert np.array_equal(got, exp)
+
+
+def test_poseidon2_known_answer_vs_pyoracle(gpu_ctx):
+    s = O.setup_from_seed()
+    from linea_stark_prover_amd.field import to_mont
+    st = to_mont([0, 1, 2]).reshape(1, 3, 4)
+    got = ints(gpu_ctx.poseidon2_permute(st)[0])
+    assert got == O.permute([0, 1, 2], s.perm)
+
+
+@pytest.mark.parametrize("w", [1, 2, 3, 4, 7, 8, 14, 23])
+def test_hash_rows_matches_sponge(gpu_ctx, oracle_lib, w):
+    rng = np.random.default_rng(w)
+    n = 300
+    rows = rand_fr(rng, (n, w))
+    got = gpu_ctx.hash_rows(rows)
+    p = oracle_params(oracle_lib)
+    exp = np.zeros((n, 4), np.uint64)
+    for i in range(n):
+        oracle_lib.lib().lo_hash_iter(ctypes.byref(p), c_ptr(rows[i]), ctypes.c_size_t(w), c_ptr(exp[i]))
+    assert np.array_equal(got, exp)
+
+
+# ---------------------------------------------------------------- Merkle
+@pytest.mark.parametrize("logh,widths", [(0, [3]), (1, [2]), (4, [8]), (10, [1, 1, 1, 1]), (12, [8]),
+                                         (13, [2]), (11, [3, 5])])
+def test_merkle_commit_open_verify(gpu_ctx, oracle_lib, logh, widths):
+    from linea_stark_prover_amd.prover import MerkleTreeMmcs
+    rng = np.random.default_rng(logh)
+    h = 1 << logh
+    mats = [rand_fr(rng, (h, w)) for w in widths]
+    mmcs = MerkleTreeMmcs(gpu_ctx)
+    root, tree = mmcs.commit(mats)
+    cat = np.concatenate(mats, axis=1).copy()
+    layers = np.zeros((2 * h - 1, 4), np.uint64)
+    p = oracle_params(oracle_lib)
+    oracle_lib.lib().lo_merkle_commit(ctypes.byref(p), c_ptr(cat), ctypes.c_size_t(h), ctypes.c_size_t(cat.shape[1]),
+                                      c_ptr(layers), 8)
+    assert np.array_equal(root.reshape(4), layers[-1])
+    assert np.array_equal(tree.layer(0), layers[:h])
+    for idx in sorted({0, h - 1, h // 3}):
+        rows, path = mmcs.open_batch(idx, tree)
+        for m, r in zip(mats, rows):
+            assert np.array_equal(r, m[idx])
+        assert mmcs.verify_batch(root, widths, logh, idx, rows, path)
+        if logh:
+            bad = path.copy()
+            bad[0, 0] ^= np.uint64(1)
+            assert not mmcs.verify_batch(root, widths, logh, idx, rows, bad)
+
+
+# ------------------------------------------------------------------- FRI
+@pytest.mark.parametrize("logn", [1, 3, 10, 14])
+def test_fri_fold_matches_pyoracle_and_fold_row(gpu_ctx, logn):
+    from linea_stark_prover_amd.prover import TwoAdicFriGenericConfig
+    from linea_stark_prover_amd.field import to_mont
+    rng = np.random.default_rng(logn)
+    n = 1 << logn
+    v = rand_fr(rng, (n,))
+    beta = rand_fr(rng, (1,))
+    g = TwoAdicFriGenericConfig(gpu_ctx)
+    got = g.fold_matrix(beta, v)
+    vi = ints(v)
+    bi = ints(beta)[0]
+    if logn <= 10:
+        assert ints(got) == O.fold_vector(vi, bi)
+    for i in sorted({0, n // 2 - 1, n // 5}):
+        e = g.fold_row(i, logn - 1, beta, v[2 * i], v[2 * i + 1])
+        assert np.array_equal(e.reshape(4), got[i])
+        assert ints(to_mont([O.fold_row(i, logn - 1, bi, vi[2 * i], vi[2 * i + 1])]))[0] == ints(got[i])[0]
+
+
+# ----------------------------------------------------------- batch inverse
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 1000, 70001])
+def test_batch_inverse(gpu_ctx, n):
+    rng = np.random.default_rng(n)
+    x = rand_fr(rng, (n,))
+    inv = gpu_ctx.batch_inverse(x)
+    xi, ii = ints(x), ints(inv)
+    for a, b in zip(xi[:2000], ii[:2000]):
+        assert a * b % P == 1
+
+
+# ---------------------------------------------------------- interpolation
+def test_interpolate_coset_matches_pyoracle(gpu_ctx):
+    from linea_stark_prover_amd.field import to_mont
+    rng = np.random.default_rng(5)
+    h, w = 16, 3
+    mat = rand_fr(rng, (h, w))
+    z = rand_fr(rng, (1,))
+    shift = to_mont([O.GENERATOR])
+    got = ints(gpu_ctx.interpolate_coset(mat, h, shift, z))
+    exp = O.interpolate_coset([ints(mat[i]) for i in range(h)], O.GENERATOR, ints(z)[0])
+    assert got == exp
+
+
+# -------------------------------------------------------------- quotient
+def _perm_setup(logn, ncols, oracle_lib):
+    s = O.setup_from_seed()
+    p = oracle_lib.setup()
+    tb, w = oracle_lib.gen_perm_trace(p, logn, ncols)
+    trace = np.frombuffer(tb.raw, dtype=np.uint64).reshape(1 << logn, w, 4).copy()
+    return s, p, trace, w
+
+
+@pytest.mark.parametrize("logn,ncols", [(3, 3), (6, 3), (5, 6), (10, 3)])
+def test_quotient_matches_oracle(gpu_ctx, oracle_lib, logn, ncols):
+    from linea_stark_prover_amd.air import permutation_air
+    s, p, trace, w = _perm_setup(logn, ncols, oracle_lib)
+    air = permutation_air(ncols)
+    proof, dbg = oracle_lib.prove(p, trace.ctypes.data, 1 << logn, w, oracle_lib.perm_air(ncols), debug=True)
+    N = (1 << logn) << 3
+    lde = np.frombuffer(dbg["trace_lde"].raw, dtype=np.uint64).reshape(N, w, 4).copy()
+    alpha = np.array(dbg["challenges"][0:4], dtype=np.uint64).reshape(1, 4)
+    pub = np.concatenate([np.array(p.alpha, np.uint64).reshape(1, 4), np.array(p.delta, np.uint64).reshape(1, 4)])
+    got = gpu_ctx.quotient_values(lde, 1 << logn, air, pub, alpha)
+    exp = np.frombuffer(dbg["quotient"].raw, dtype=np.uint64).reshape(-1, 4)
+    assert np.array_equal(got, exp)
+
+
+# ------------------------------------------------------------ full prove
+def _pub(p):
+    return np.concatenate([np.array(p.alpha, np.uint64).reshape(1, 4), np.array(p.delta, np.uint64).reshape(1, 4)])
+
+
+@pytest.mark.parametrize("logn,ncols", [(1, 3), (2, 3), (3, 3), (4, 6), (8, 3), (11, 3), (12, 6), (13, 3)])
+def test_prove_bit_exact_vs_oracle(gpu_ctx, oracle_lib, logn, ncols):
+    from linea_stark_prover_amd.air import permutation_air
+    s, p, trace, w = _perm_setup(logn, ncols, oracle_lib)
+    air = permutation_air(ncols)
+    pub = _pub(p)
+    got = gpu_ctx.prove(trace, air, pub)
+    exp = oracle_lib.prove(p, trace.ctypes.data, 1 << logn, w, oracle_lib.perm_air(ncols))
+    assert got == exp
+    assert gpu_ctx.verify(got, air, pub)
+    assert oracle_lib.verify(p, got, oracle_lib.perm_air(ncols)) == 0
+
+
+def test_prove_tiny_vs_pyoracle(gpu_ctx, oracle_lib):
+    from linea_stark_prover_amd.air import permutation_air
+    s, p, trace, w = _perm_setup(3, 3, oracle_lib)
+    cfgs, cols = O.synthetic_perm_trace(3, 3, s.alpha, s.delta, O.DEFAULT_SEED)
+    pf = O.prove(cfgs, O.columns_to_rows(cols), [s.alpha, s.delta], s.perm)
+    assert gpu_ctx.prove(trace, permutation_air(3), _pub(p)) == O.serialize_proof(pf)
+
+
+def test_prove_lookup_and_permutation_air(gpu_ctx, oracle_lib):
+    """Wide-AIR shape: LogUp lookup config + permutation config in one trace."""
+    from linea_stark_prover_amd.air import AirLookupConfig, AirPermutationConfig, LineaAIR
+    from linea_stark_prover_amd.field import to_mont
+    s = O.setup_from_seed()
+    p = oracle_lib.setup()
+    rng = O.SplitMix64(99)
+    n = 64
+    tab = [[rng.sample_fr() for _ in range(n)] for _ in range(3)]
+    tab2 = [[rng.sample_fr() for _ in range(n)] for _ in range(3)]
+    a = [[0] * n for _ in range(3)]
+    for i in range(n):
+        j = rng.below(n)
+        src = tab if i % 3 else tab2
+        for c in range(3):
+            a[c][i] = src[c][j]
+    af = [1] * n
+    af[5] = 0
+    cfg, cols = O.lookup_witness(a, [tab, tab2], af, [[1] * n, [1] * n], s.alpha, s.delta)
+    pc, pcols = O.synthetic_perm_trace(6, 3, s.alpha, s.delta, 5)
+    cfgs = [cfg, O.shift_cfg(pc[0], len(cols))]
+    rows = O.columns_to_rows(cols + pcols)
+    w = len(rows[0])
+    trace = to_mont([x for r in rows for x in r]).reshape(n, w, 4)
+    c0, c1 = cfgs
+    air = LineaAIR([AirLookupConfig(c0.a_cols, c0.b_cols, c0.a_filter, c0.b_filter, c0.a_inv, c0.b_inv, c0.occ,
+                                    c0.check),
+                    AirPermutationConfig(c1.a_cols, c1.b_cols, c1.b_inv, c1.check)])
+    assert air.descriptor() == oracle_lib.air_desc(cfgs)
+    got = gpu_ctx.prove(trace, air, _pub(p))
+    exp = oracle_lib.prove(p, trace.ctypes.data, n, w, oracle_lib.air_desc(cfgs))
+    assert got == exp
+    assert gpu_ctx.verify(got, air, _pub(p))
+
+
+def test_prove_rejects_tampering(gpu_ctx, oracle_lib):
+    from linea_stark_prover_amd.air import permutation_air
+    s, p, trace, w = _perm_setup(6, 3, oracle_lib)
+    air = permutation_air(3)
+    pf = bytearray(gpu_ctx.prove(trace, air, _pub(p)))
+    for off in (8 + 20 + 5, 8 + 20 + 64 + 7, len(pf) // 2, len(pf) - 3):
+        bad = bytearray(pf)
+        bad[off] ^= 1
+        assert not gpu_ctx.verify(bytes(bad), air, _pub(p))
+
+
+def test_prove_large_self_consistency(gpu_ctx):
+    """2^16 rows: no oracle at this size in the default run; the product's
+    verifier must accept and the LDE must agree with the trace on the low
+    coset's defining property (re-proving is deterministic)."""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import gen_permutation_trace
+    a, d, _ = gpu_ctx.config.seeded()
+    tr = gen_permutation_trace(16, 3, a, d)
+    pub = np.concatenate([a, d])
+    air = permutation_air(3)
+    pf1 = gpu_ctx.prove(tr, air, pub)
+    pf2 = gpu_ctx.prove(tr, air, pub)
+    assert pf1 == pf2
+    assert gpu_ctx.verify(pf1, air, pub)

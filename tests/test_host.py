@@ -1,0 +1,152 @@
+"""CPU-only tests of the product library: it loads, exports every symbol of
+include/lsp.h, and its host logic (seeded setup, witness generation, AIR
+descriptor + degree rule, field helpers, the CPU verifier) agrees with the
+oracle.  No compute call here touches a GPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "lsp.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(lsp_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol(product_lib):
+    syms = header_symbols()
+    assert len(syms) >= 30
+    for s in syms:
+        assert hasattr(product_lib, s), f"{s} declared in include/lsp.h but not exported"
+    from linea_stark_prover_amd import _lib
+    assert sorted(_lib.EXPORTED) == syms
+
+
+def test_version(product_lib):
+    assert b"gfx950" in product_lib.lsp_version()
+
+
+def test_seeded_setup_matches_oracle(product_lib):
+    from linea_stark_prover_amd.field import from_mont
+    from linea_stark_prover_amd.prover import StarkConfig
+    a, d, rc = StarkConfig().seeded()
+    s = O.setup_from_seed()
+    assert from_mont(a)[0] == s.alpha and from_mont(d)[0] == s.delta
+    flat = [x for r in s.perm.ext_initial for x in r] + [x for r in s.perm.ext_terminal for x in r] + s.perm.internal
+    assert from_mont(rc) == flat
+
+
+@pytest.mark.parametrize("logn,ncols,small", [(3, 3, False), (6, 6, False), (5, 3, True)])
+def test_gen_permutation_trace_matches_oracle(product_lib, logn, ncols, small):
+    from linea_stark_prover_amd.field import from_mont
+    from linea_stark_prover_amd.prover import StarkConfig, gen_permutation_trace
+    a, d, _ = StarkConfig().seeded()
+    tr = gen_permutation_trace(logn, ncols, a, d, small_values=small)
+    s = O.setup_from_seed()
+    cfgs, cols = O.synthetic_perm_trace(logn, ncols, s.alpha, s.delta, O.DEFAULT_SEED, small=small)
+    rows = O.columns_to_rows(cols)
+    assert from_mont(tr.reshape(-1, 4)) == [x for r in rows for x in r]
+
+
+def test_field_helpers(product_lib):
+    from linea_stark_prover_amd.field import from_mont, to_mont
+    L = product_lib
+    vals = [0, 1, 2, O.P - 1, 12345678901234567890, O.P // 3]
+    m = to_mont(vals)
+    for i, v in enumerate(vals):
+        can = np.zeros(4, np.uint64)
+        L.lsp_fr_to_canonical(m[i].ctypes.data, can.ctypes.data)
+        assert int.from_bytes(can.tobytes(), "little") == v
+        back = np.zeros(4, np.uint64)
+        L.lsp_fr_from_canonical(can.ctypes.data, back.ctypes.data)
+        assert np.array_equal(back, m[i])
+    a, b = to_mont([O.P - 5]), to_mont([987654321])
+    out = np.zeros((1, 4), np.uint64)
+    L.lsp_fr_mul(a.ctypes.data, b.ctypes.data, out.ctypes.data)
+    assert from_mont(out)[0] == (O.P - 5) * 987654321 % O.P
+    L.lsp_fr_inv(b.ctypes.data, out.ctypes.data)
+    assert from_mont(out)[0] * 987654321 % O.P == 1
+    for bits in (0, 1, 3, 19, 47):
+        L.lsp_two_adic_generator(bits, out.ctypes.data)
+        assert from_mont(out)[0] == O.two_adic_generator(bits)
+    be = bytes(range(32))
+    L.lsp_fr_from_be_bytes_mod_order(be, 32, out.ctypes.data)
+    assert from_mont(out)[0] == O.from_be_bytes_mod_order(be)
+
+
+def test_air_descriptor_and_degree_rule(product_lib):
+    from linea_stark_prover_amd import _lib
+    from linea_stark_prover_amd.air import AirLookupConfig, LineaAIR, permutation_air
+    from oracle import cref
+    for ncols in (1, 3, 6, 12):
+        air = permutation_air(ncols)
+        cfgs = [O.PermCfg(list(range(ncols)), list(range(ncols, 2 * ncols)), 2 * ncols, 2 * ncols + 1)]
+        assert air.descriptor() == cref.air_desc(cfgs)
+        for pd in (0, 1):
+            d = (ctypes.c_int32 * len(air.descriptor()))(*air.descriptor())
+            lq = ctypes.c_uint32()
+            assert product_lib.lsp_log_quotient_degree(d, len(d), pd, ctypes.byref(lq)) == 0
+            assert lq.value == O.log_quotient_degree(cfgs, pd)
+    # 3+3 -> 4 chunks, 6+6 -> 8 chunks under the default (fork) rule: SURVEY 0.6 #2
+    assert O.log_quotient_degree([O.PermCfg([0, 1, 2], [3, 4, 5], 6, 7)]) == 2
+    assert O.log_quotient_degree([O.PermCfg(list(range(6)), list(range(6, 12)), 12, 13)]) == 3
+    lk = AirLookupConfig([0, 1], [[2, 3], [4, 5]], 6, [7, 8], 9, [10, 11], [12, 13], 14)
+    assert lk.width() == 15
+    bad = (ctypes.c_int32 * 3)(1, 9, 0)
+    lq = ctypes.c_uint32()
+    assert product_lib.lsp_log_quotient_degree(bad, 3, 1, ctypes.byref(lq)) == _lib.LSP_E_ARG
+
+
+@pytest.fixture(scope="module")
+def host_ctx(product_lib):
+    from linea_stark_prover_amd import _lib
+    from linea_stark_prover_amd.prover import Context, StarkConfig
+    return Context(StarkConfig(), device=-1)
+
+
+def test_host_only_context_rejects_device_calls(host_ctx):
+    from linea_stark_prover_amd import _lib
+    with pytest.raises(_lib.LspError) as e:
+        host_ctx.hash_rows(np.zeros((4, 2, 4), np.uint64))
+    assert e.value.code == _lib.LSP_E_STATE
+
+
+@pytest.mark.parametrize("logn,ncols", [(3, 3), (5, 6), (7, 3)])
+def test_product_verifier_accepts_oracle_proofs(host_ctx, oracle_lib, logn, ncols):
+    """The product's CPU verifier (lsp_verify) accepts proofs made by the C
+    oracle and rejects single-bit mutations."""
+    from linea_stark_prover_amd.air import permutation_air
+    p = oracle_lib.setup()
+    tb, w = oracle_lib.gen_perm_trace(p, logn, ncols)
+    proof = oracle_lib.prove(p, tb, 1 << logn, w, oracle_lib.perm_air(ncols))
+    pub = np.concatenate([np.array(p.alpha, np.uint64).reshape(1, 4), np.array(p.delta, np.uint64).reshape(1, 4)])
+    air = permutation_air(ncols)
+    assert host_ctx.verify(proof, air, pub)
+    rng = np.random.default_rng(logn)
+    for off in rng.integers(28, len(proof), 6):
+        bad = bytearray(proof)
+        bad[int(off)] ^= 1 << int(rng.integers(0, 8))
+        assert not host_ctx.verify(bytes(bad), air, pub)
+    # wrong public values
+    pub2 = pub.copy()
+    pub2[1, 0] ^= np.uint64(1)
+    assert not host_ctx.verify(proof, air, pub2)
+
+
+def test_fold_row_host_matches_pyoracle(product_lib):
+    from linea_stark_prover_amd.field import from_mont, to_mont
+    from linea_stark_prover_amd.prover import TwoAdicFriGenericConfig
+    rng = O.SplitMix64(3)
+    for logh in (0, 1, 5, 12):
+        for _ in range(3):
+            idx = rng.below(1 << logh)
+            b, e0, e1 = rng.sample_fr(), rng.sample_fr(), rng.sample_fr()
+            got = TwoAdicFriGenericConfig.fold_row(idx, logh, to_mont([b]), to_mont([e0]), to_mont([e1]))
+            assert from_mont(got)[0] == O.fold_row(idx, logh, b, e0, e1)

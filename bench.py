@@ -1,0 +1,186 @@
+"""Headline benchmark: prove time + trace rows/s of the 3x3 permutation AIR.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--log-n 19] [--ncols 3]
+
+A "step" is one full ``p3_uni_stark::prove`` (bin/src/main.rs:80-86) of the
+3x3 permutation AIR (3 'from' + 3 'to' columns + b_inverse + check, w = 8,
+4 quotient chunks, log_blowup 3, 33 queries) on one synthetic 2^log_n-row
+trace that is already resident in HBM, ending with the serialized proof on
+the host.  For N > 1 (launched by torch.distributed.run) every rank proves its
+own independent trace (replicas, no data-path collective);
+``value`` = all rows proven by all ranks / the max-over-ranks wall time.
+
+Besides the contract fields the JSON line carries:
+  roofline       the coset LDE (the metric's "NTT HBM GB/s"): algorithmic
+                 bytes 32*w*(h + N) per coset_lde_batch / its event-timed
+                 duration, vs the 8 TB/s HBM3E peak
+  roofline_valu  the dominant kernel family (Poseidon2 Merkle hashing):
+                 algorithmic Fr multiplications / time vs the Fr-mul peak
+                 of the same multiplier measured by lsp_calibrate_fr_mul
+  cpu_baseline   the C restatement (oracle/, "port") proving a bounded
+                 sample on the host cores, rank 0 at N = 1 only
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "prove time (s) + trace-rows/sec, 3x3 perm AIR @2^19; NTT HBM GB/s vs roofline"
+PUBLISHED_ROWS_PER_S = 524288 / 330.0  # README.md:11 (~330 s for 2^19 rows, CPU)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--log-n", type=int, default=19)
+    ap.add_argument("--ncols", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=0x4C494E4541)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-log-n", type=int, default=17, help="bounded CPU-baseline sample size")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        # control plane only (barrier + max-over-ranks of the wall time): the
+        # proofs are independent replicas, no data-path collective.  torch is
+        # imported before liblsp_hip.so so one HIP runtime serves the process.
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
+
+    import numpy as np
+
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import Context, StarkConfig, gen_permutation_trace
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    cfg = StarkConfig(seed=args.seed)
+    ctx = Context(cfg, device=local)
+    a, d, _ = cfg.seeded()
+    pub = np.concatenate([a, d])
+    air = permutation_air(args.ncols)
+    h = 1 << args.log_n
+    w = 2 * args.ncols + 2
+    trace = gen_permutation_trace(args.log_n, args.ncols, a, d, seed=args.seed + rank)
+    dtrace = ctx.dev_alloc(trace.nbytes)
+    ctx.h2d(dtrace, trace)
+
+    proof = None
+    for _ in range(args.warmup):
+        proof = ctx.prove(dtrace, air, pub, h, w)
+    phases_acc = {}
+    barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        proof = ctx.prove(dtrace, air, pub, h, w)
+        for name, ms in ctx.last_timings():
+            phases_acc[name] = phases_acc.get(name, 0.0) + ms
+    ctx.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    phases = {k: v / max(args.steps, 1) for k, v in phases_acc.items()}
+    verified = ctx.verify(proof, air, pub) if proof is not None else False
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = world * h * args.steps / elapsed
+        N = h << cfg.log_blowup
+        q = 4 if args.ncols <= 3 else 8
+        lde_ms = phases.get("coset_lde_batch", float("nan"))
+        lde_bytes = 32 * w * (h + N)
+        achieved = lde_bytes / (lde_ms * 1e-3) / 1e9
+        # Poseidon2 Merkle work of one proof (SURVEY 8(d) perm-count formula)
+        perms = N * ((w + 1) // 2) + (N - 1) + N * ((q + 1) // 2) + (N - 1)
+        L = N
+        while L > (1 << cfg.log_blowup):
+            perms += L // 2 + (L // 2 - 1)
+            L //= 2
+        merkle_ms = phases.get("merkle tree", float("nan"))
+        trace_perms = N * ((w + 1) // 2) + (N - 1)
+        mul_per_perm = 230
+        calib = ctx.calibrate_fr_mul() if hasattr(ctx, "calibrate_fr_mul") else None
+        valu_achieved = trace_perms * mul_per_perm / (merkle_ms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "trace-rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "prove_time_s": ms_per_step / 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": value / PUBLISHED_ROWS_PER_S,
+            "baseline_published": {"value": PUBLISHED_ROWS_PER_S, "unit": "trace-rows/s",
+                                   "source": "reference README.md:11, ~330 s for 2^19 rows on a 16-core CPU"},
+            "dtype": "fr253 (BLS12-377 Fr, 8x u32 Montgomery limbs)",
+            "data": "synthetic (seeded permutation trace, SURVEY 8(d) C1)",
+            "config": {"workload": f"{args.ncols}x{args.ncols} permutation AIR, 2^{args.log_n} rows "
+                                   f"(w={w}, q={q} quotient chunks, log_blowup {cfg.log_blowup}, "
+                                   f"{cfg.num_queries} queries, Poseidon2-w3 Merkle, FRI)",
+                       "log_n": args.log_n, "width": w, "fri_queries": cfg.num_queries,
+                       "parallelism": "replicas" if world > 1 else "single-gpu"},
+            "verified": bool(verified),
+            "phases_ms": {k: round(v, 3) for k, v in phases.items()},
+            "roofline": {"bound": "hbm", "kernel": "coset_lde_batch (trace, w x 2^log_n -> 8x)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes": lde_bytes, "ms": lde_ms},
+            "roofline_valu": {"bound": "valu", "kernel": "trace Merkle tree (Poseidon2 leaf hash + levels)",
+                              "achieved": valu_achieved, "unit": "G Fr-mul/s",
+                              "peak": calib, "frac": (valu_achieved / calib) if calib else None,
+                              "perms": trace_perms, "mul_per_perm": mul_per_perm, "ms": merkle_ms},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(out), flush=True)
+    ctx.dev_free(dtrace)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args):
+    """The oracle's C restatement proving a bounded sample of the same workload
+    on the host (test infrastructure used only as the reported baseline)."""
+    from oracle import cref
+    cref.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    p = cref.setup(args.seed)
+    tb, w = cref.gen_perm_trace(p, args.cpu_log_n, args.ncols, seed=args.seed)
+    t = time.perf_counter()
+    cref.prove(p, tb, 1 << args.cpu_log_n, w, cref.perm_air(args.ncols), nthreads=threads)
+    dt = time.perf_counter() - t
+    return {"value": (1 << args.cpu_log_n) / dt, "unit": "trace-rows/s", "cores": threads, "kind": "port",
+            "seconds": dt,
+            "sample": f"oracle/lsp_oracle.c full prove, {args.ncols}x{args.ncols} permutation AIR at "
+                      f"2^{args.cpu_log_n} rows (same conventions/seed), {threads} threads"}
+
+
+if __name__ == "__main__":
+    main()

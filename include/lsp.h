@@ -189,6 +189,11 @@ int lsp_verify(const lsp_ctx *ctx, const int32_t *air, size_t air_len, const lsp
  * reference's bench.log */
 int lsp_last_timings(const lsp_ctx *ctx, double *ms, const char **names, size_t cap, size_t *n);
 
+/* Fr-multiplication throughput of the device multiplier (register-resident
+ * independent chains): the calibrated VALU peak the Merkle/Poseidon2
+ * roofline is quoted against. */
+int lsp_calibrate_fr_mul(lsp_ctx *ctx, double *gmul_per_s);
+
 /* ------------------------------------------------------------- witness */
 /* Synthetic permutation trace with the witness columns of
  * RawPermutationTrace::get_trace (trace/src/permutation.rs:24-93):

@@ -576,6 +576,30 @@ int lsp_last_timings(const lsp_ctx* ctx, double* ms, const char** names, size_t 
     return LSP_OK;
 }
 
+int lsp_calibrate_fr_mul(lsp_ctx* ctx, double* gmul_per_s) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(gmul_per_s, LSP_E_ARG, "null");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const size_t nth = 256 * 256 * 16;  // 16 blocks of 256 lanes per CU
+        const uint32_t iters = 256;
+        Fr* out = ctx->fbuf("calib", nth);
+        LSP_HIP(launch_calib_mul(out, nth, 8, ctx->stream));  // warm
+        hipEvent_t e0, e1;
+        LSP_HIP(hipEventCreate(&e0));
+        LSP_HIP(hipEventCreate(&e1));
+        LSP_HIP(hipEventRecord(e0, ctx->stream));
+        LSP_HIP(launch_calib_mul(out, nth, iters, ctx->stream));
+        LSP_HIP(hipEventRecord(e1, ctx->stream));
+        LSP_HIP(hipEventSynchronize(e1));
+        float ms = 0;
+        LSP_HIP(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        *gmul_per_s = (double)nth * iters * 4 / (ms * 1e-3) / 1e9;
+    });
+}
+
 int lsp_gen_permutation_trace(uint64_t seed, uint32_t log_n, uint32_t ncols, const lsp_fr* alpha,
                               const lsp_fr* delta, int small_values, lsp_fr* rows) {
     return guarded(nullptr, [&] {

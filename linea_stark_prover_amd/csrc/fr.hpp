@@ -135,7 +135,8 @@ LSP_HD Fr fr_sub(const Fr& a, const Fr& b) {
 LSP_HD Fr fr_neg(const Fr& a) { return fr_sub(fr_zero(), a); }
 LSP_HD Fr fr_dbl(const Fr& a) { return fr_add(a, a); }
 
-LSP_HD Fr fr_mul(const Fr& a, const Fr& b) {
+// Portable CIOS (host, and the reference point of the device multiplier)
+LSP_HD Fr fr_mul_cios(const Fr& a, const Fr& b) {
     uint32_t t[8];
     // i = 0 (t = 0)
     {
@@ -179,6 +180,20 @@ LSP_HD Fr fr_mul(const Fr& a, const Fr& b) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) r.v[i] = t[i];
     return fr_reduce_once(r);
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// gfx950 device product: FIPS with one inline-asm block per column
+// (generated by tools/gen_frmul.py)
+#include "fr_mul_gfx950.inc"
+#endif
+
+LSP_HD Fr fr_mul(const Fr& a, const Fr& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return fr_mul_dev(a, b);
+#else
+    return fr_mul_cios(a, b);
+#endif
 }
 
 LSP_HD Fr fr_sqr(const Fr& a) { return fr_mul(a, a); }

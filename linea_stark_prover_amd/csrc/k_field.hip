@@ -31,6 +31,20 @@ __global__ __launch_bounds__(256) void k_batch_inverse(const Fr* __restrict__ in
     }
 }
 
+// Fr-mul throughput probe: 4 independent register-resident chains per lane
+__global__ __launch_bounds__(256) void k_calib_mul(Fr* __restrict__ out, uint32_t iters) {
+    const size_t t = gtid();
+    Fr a = fr_from_u64(t + 3), b = fr_from_u64(t * 7 + 5), c = fr_from_u64(t + 11), d = fr_from_u64(t + 13);
+    const Fr m = fr_from_u64(0x1234567u + (uint32_t)t);
+    for (uint32_t i = 0; i < iters; ++i) {
+        a = fr_mul(a, m);
+        b = fr_mul(b, m);
+        c = fr_mul(c, m);
+        d = fr_mul(d, m);
+    }
+    out[t] = fr_add(fr_add(a, b), fr_add(c, d));
+}
+
 __global__ __launch_bounds__(256) void k_gather(const uint64_t* __restrict__ ptrs, Fr* __restrict__ out, size_t n) {
     const size_t i = gtid();
     if (i < n) out[i] = *reinterpret_cast<const Fr*>(ptrs[i]);
@@ -41,6 +55,11 @@ hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st)
     if (!n) return hipSuccess;
     const size_t T = (n + BINV_CHUNK - 1) / BINV_CHUNK;
     hipLaunchKernelGGL(k_batch_inverse, dim3(nblocks(T, 256)), dim3(256), 0, st, in, out, n, T);
+    return hipGetLastError();
+}
+
+hipError_t launch_calib_mul(Fr* out, size_t nthreads, uint32_t iters, hipStream_t st) {
+    hipLaunchKernelGGL(k_calib_mul, dim3(nblocks(nthreads, 256)), dim3(256), 0, st, out, iters);
     return hipGetLastError();
 }
 

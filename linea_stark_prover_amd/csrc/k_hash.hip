@@ -60,12 +60,12 @@ __global__ __launch_bounds__(256) void k_merkle_level(const Fr* __restrict__ src
     dst[i] = compress2<D>(src[2 * i], src[2 * i + 1], rc, rf, rp);
 }
 
-// Top of a tree in one workgroup: `len` (<= 1024, power of two) digests at
+// Top of a tree in one workgroup: `len` (<= 2*blockDim, power of two) digests at
 // layers[off..off+len) -> every layer above them, through the LDS.
 template <uint32_t D>
-__global__ __launch_bounds__(512) void k_merkle_top(Fr* __restrict__ layers, size_t off, uint32_t len,
+__global__ __launch_bounds__(64) void k_merkle_top(Fr* __restrict__ layers, size_t off, uint32_t len,
                                                     const Fr* __restrict__ rc, uint32_t rf, uint32_t rp) {
-    __shared__ Fr buf[1024];
+    __shared__ Fr buf[128];
     for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) buf[e] = layers[off + e];
     __syncthreads();
     size_t out_off = off + len;
@@ -101,11 +101,12 @@ hipError_t launch_permute(Fr* states, size_t n, const Fr* rc, P2Layout L, hipStr
 
 hipError_t launch_hash_rows(const MatList& m, size_t nrows, Fr* out, const Fr* rc, P2Layout L, hipStream_t st) {
     if (!nrows) return hipSuccess;
+    const unsigned bs = nrows >= (1u << 14) ? 256u : 64u;  // spread narrow batches over more CUs
     if (m.n == 1)
-        LSP_DISPATCH_D(L, k_hash_rows1, dim3(nblocks(nrows, 256)), dim3(256), 0, st, m.ptr[0], m.width[0], nrows,
+        LSP_DISPATCH_D(L, k_hash_rows1, dim3(nblocks(nrows, bs)), dim3(bs), 0, st, m.ptr[0], m.width[0], nrows,
                        out, rc, L.rounds_f, L.rounds_p);
     else
-        LSP_DISPATCH_D(L, k_hash_rows_multi, dim3(nblocks(nrows, 256)), dim3(256), 0, st, m, nrows, out, rc,
+        LSP_DISPATCH_D(L, k_hash_rows_multi, dim3(nblocks(nrows, bs)), dim3(bs), 0, st, m, nrows, out, rc,
                        L.rounds_f, L.rounds_p);
     return hipGetLastError();
 }
@@ -118,15 +119,23 @@ hipError_t launch_merkle_level(const Fr* src, Fr* dst, size_t nout, const Fr* rc
 }
 
 hipError_t launch_merkle_tree(Fr* layers, size_t nleaves, const Fr* rc, P2Layout L, hipStream_t st) {
+    // Wide levels: one compression per lane, 256-lane blocks.  Narrow levels
+    // (< 2^14 nodes) are latency-bound (one permutation per level on the
+    // critical path): 64-lane blocks spread their waves over as many CUs as
+    // possible.  The last 64 -> 1 levels run in one wave.
     size_t off = 0, len = nleaves;
-    while (len > 1024) {
-        hipError_t e = launch_merkle_level(layers + off, layers + off + len, len / 2, rc, L, st);
+    while (len > 64) {
+        const size_t nout = len / 2;
+        const unsigned bs = nout >= (1u << 14) ? 256u : 64u;
+        LSP_DISPATCH_D(L, k_merkle_level, dim3(nblocks(nout, bs)), dim3(bs), 0, st, layers + off, layers + off + len,
+                       nout, rc, L.rounds_f, L.rounds_p);
+        hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
         off += len;
         len /= 2;
     }
     if (len > 1) {
-        LSP_DISPATCH_D(L, k_merkle_top, dim3(1), dim3(512), 0, st, layers, off, (uint32_t)len, rc, L.rounds_f,
+        LSP_DISPATCH_D(L, k_merkle_top, dim3(1), dim3(64), 0, st, layers, off, (uint32_t)len, rc, L.rounds_f,
                        L.rounds_p);
         return hipGetLastError();
     }

@@ -47,6 +47,8 @@ hipError_t launch_merkle_tree(Fr* layers, size_t nleaves, const Fr* rc, P2Layout
 // --------------------------------------------------------- k_field.hip
 // out[i] = 1 / in[i] (Montgomery trick, interleaved chunks); in may alias out? no
 hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st);
+// Fr-mul throughput probe: nthreads lanes x iters x 4 independent products
+hipError_t launch_calib_mul(Fr* out, size_t nthreads, uint32_t iters, hipStream_t st);
 // out[i] = *ptrs[i]
 hipError_t launch_gather(const uint64_t* ptrs, Fr* out, size_t n, hipStream_t st);
 

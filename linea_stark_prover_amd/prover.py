@@ -204,6 +204,12 @@ class Context:
         L.check(rc)
         return True
 
+    def calibrate_fr_mul(self) -> float:
+        """G Fr-mul/s of the device multiplier (register-resident chains)."""
+        v = ctypes.c_double()
+        self._chk(L.lib().lsp_calibrate_fr_mul(self.h, ctypes.byref(v)))
+        return v.value
+
     def last_timings(self) -> List[Tuple[str, float]]:
         n = ctypes.c_size_t()
         L.lib().lsp_last_timings(self.h, None, None, 0, ctypes.byref(n))

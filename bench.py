@@ -51,26 +51,14 @@ def parse():
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        # control plane only (barrier + max-over-ranks of the wall time): the
-        # proofs are independent replicas, no data-path collective.  torch is
-        # imported before liblsp_hip.so so one HIP runtime serves the process.
-        import torch
-        import torch.distributed as dist
-        dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
+    from linea_stark_prover_amd.replicas import init_from_env, rank_seed, timed_steps
+    dist = init_from_env()  # gloo control plane when WORLD_SIZE > 1 (imports torch first)
+    world, rank, local = dist.world, dist.rank, dist.local_rank
 
     import numpy as np
 
     from linea_stark_prover_amd.air import permutation_air
     from linea_stark_prover_amd.prover import Context, StarkConfig, gen_permutation_trace
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
 
     cfg = StarkConfig(seed=args.seed)
     ctx = Context(cfg, device=local)
@@ -79,29 +67,18 @@ def main():
     air = permutation_air(args.ncols)
     h = 1 << args.log_n
     w = 2 * args.ncols + 2
-    trace = gen_permutation_trace(args.log_n, args.ncols, a, d, seed=args.seed + rank)
+    trace = gen_permutation_trace(args.log_n, args.ncols, a, d, seed=rank_seed(args.seed, rank))
     dtrace = ctx.dev_alloc(trace.nbytes)
-    ctx.h2d(dtrace, trace)
+    ctx.h2d(dtrace, trace)  # resident in HBM before the timed region
 
-    proof = None
-    for _ in range(args.warmup):
-        proof = ctx.prove(dtrace, air, pub, h, w)
     phases_acc = {}
-    barrier()
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        proof = ctx.prove(dtrace, air, pub, h, w)
+
+    def record():
         for name, ms in ctx.last_timings():
             phases_acc[name] = phases_acc.get(name, 0.0) + ms
-    ctx.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+
+    elapsed, proof = timed_steps(lambda: ctx.prove(dtrace, air, pub, h, w), args.steps, args.warmup, dist,
+                                 sync=ctx.synchronize, on_step=record)
     phases = {k: v / max(args.steps, 1) for k, v in phases_acc.items()}
     verified = ctx.verify(proof, air, pub) if proof is not None else False
 
@@ -161,8 +138,7 @@ def main():
         print(json.dumps(out), flush=True)
     ctx.dev_free(dtrace)
     ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    dist.close()
 
 
 def cpu_baseline(args):

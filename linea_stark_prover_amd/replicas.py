@@ -1,0 +1,77 @@
+"""Multi-GPU control plane for independent proofs ("replicas").
+
+One process per GPU (launched by torch.distributed.run). Every rank proves its
+own trace; the only cross-rank traffic is a barrier before and after the timed
+region and a MAX-reduction of the wall time (gloo, CPU tensors). There is no
+data-path collective because independent proofs share nothing.
+
+torch is imported before liblsp_hip.so is loaded so that a single HIP runtime
+(the one torch ships, same SONAME) serves the process.
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+
+@dataclass
+class Dist:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    pg: Optional[object] = None   # torch.distributed module when world > 1
+
+    def barrier(self):
+        if self.pg is not None:
+            self.pg.barrier()
+
+    def max(self, x: float) -> float:
+        if self.pg is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.pg is not None:
+            self.pg.destroy_process_group()
+            self.pg = None
+
+
+def init_from_env() -> Dist:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world <= 1:
+        return Dist(rank, world, local, None)
+    import torch  # noqa: F401  (before the HIP library: one runtime per process)
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
+    return Dist(rank, world, local, dist)
+
+
+def timed_steps(step: Callable[[], object], steps: int, warmup: int, d: Dist,
+                sync: Callable[[], None] = lambda: None, on_step: Callable[[], None] = lambda: None):
+    """W untimed steps, barrier + sync, K timed steps, sync + barrier; returns
+    (max-over-ranks elapsed seconds, last step result)."""
+    out = None
+    for _ in range(warmup):
+        out = step()
+    d.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = step()
+        on_step()
+    sync()
+    d.barrier()
+    return d.max(time.perf_counter() - t0), out
+
+
+def rank_seed(base_seed: int, rank: int) -> int:
+    """Each replica proves a distinct synthetic trace."""
+    return base_seed + rank

@@ -159,6 +159,9 @@ int lsp_ctx_create(int device, const lsp_params* p, lsp_ctx** out) {
             LSP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
             LSP_HIP(hipMalloc(&c->rc_dev, nrc * sizeof(Fr)));
             LSP_HIP(hipMemcpy(c->rc_dev, c->p2.rc.data(), nrc * sizeof(Fr), hipMemcpyHostToDevice));
+            LSP_HIP(hipMalloc(&c->rc29_dev, nrc * sizeof(F29)));
+            LSP_HIP(launch_rc_to_f29(c->rc_dev, c->rc29_dev, (uint32_t)nrc, c->stream));
+            LSP_HIP(hipStreamSynchronize(c->stream));
         }
         c->log_blowup = p->log_blowup;
         c->log_final_poly_len = p->log_final_poly_len;
@@ -181,6 +184,7 @@ int lsp_ctx_destroy(lsp_ctx* ctx) {
         if (kv.second.p) (void)hipFree(kv.second.p);
     for (auto& kv : ctx->twiddles) (void)hipFree(kv.second);
     if (ctx->rc_dev) (void)hipFree(ctx->rc_dev);
+    if (ctx->rc29_dev) (void)hipFree(ctx->rc29_dev);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return LSP_OK;
@@ -251,7 +255,7 @@ int lsp_poseidon2_permute_batch(lsp_ctx* ctx, lsp_fr* states, size_t n, int mem)
         std::lock_guard<std::mutex> g(ctx->mu);
         need_gpu(ctx);
         Fr* d = const_cast<Fr*>(dev_in(ctx, states, 3 * n, mem, "api_in"));
-        LSP_HIP(launch_permute(d, n, ctx->rc_dev, ctx->p2.L, ctx->stream));
+        LSP_HIP(launch_permute(d, n, ctx->rc29_dev, ctx->p2.L, ctx->stream));
         finish_out(ctx, states, d, 3 * n, mem);
     });
 }
@@ -267,7 +271,7 @@ int lsp_hash_rows(lsp_ctx* ctx, const lsp_fr* rows, size_t n, size_t w, lsp_fr* 
         m.ptr[0] = din;
         m.width[0] = (uint32_t)w;
         m.n = 1;
-        LSP_HIP(launch_hash_rows(m, n, dout, ctx->rc_dev, ctx->p2.L, ctx->stream));
+        LSP_HIP(launch_hash_rows(m, n, dout, ctx->rc29_dev, ctx->p2.L, ctx->stream));
         finish_out(ctx, out, dout, n, mem);
     });
 }

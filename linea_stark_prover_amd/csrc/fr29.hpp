@@ -1,0 +1,186 @@
+// Fr in 9 x 29-bit limbs on gfx950: the Poseidon2 working representation.
+//
+// Why: with 29-bit limbs every 29x29-bit product is < 2^58, so a whole
+// FIPS column (at most 9 + 8 products plus the carry) fits in one 64-bit
+// accumulator: each product is a single v_mad_u64_u32 with no carry-out to
+// fold (the 32-bit-limb FIPS needs a v_addc_co_u32 after every product).
+// 153 mads per product instead of 121 mads + 120 adds.
+//
+// Representation: x is held as X = x * 2^261 mod r ("Montgomery, R' = 2^261")
+// in limbs l[0..8] of 29 bits (l[8] may hold a few more bits).  Values are
+// kept lazily reduced; the invariants (see fr29_mul) are
+//   mul inputs  < 32 r with normalised limbs  ->  mul output < 3.3 r,
+// and values < 8 r whenever they come from the adders below.
+// Conversions to/from the ark-ff form (x * 2^256 mod r, 8 x 32-bit limbs):
+// from: repack bits, Montgomery-multiply by 2^266 mod r (x 2^5);
+// to:   Montgomery-multiply by 2^256 mod r (x 2^-5), reduce to [0, r), repack.
+#pragma once
+#include "fr.hpp"
+
+namespace lsp {
+
+struct F29 {
+    uint32_t l[9];
+};
+
+#define F29_MASK 0x1fffffffu
+
+// r in 29-bit limbs: r[0] = 1 (r = 1 mod 2^47), r[2] = 0x42
+__device__ __forceinline__ constexpr uint32_t p29(int i) {
+    return i == 0 ? 0x1u
+         : i == 1 ? 0x108c0000u
+         : i == 2 ? 0x42u
+         : i == 3 ? 0x14edfda0u
+         : i == 4 ? 0x1b00159au
+         : i == 5 ? 0x68f2e1bu
+         : i == 6 ? 0x155982d1u
+         : i == 7 ? 0xbd34594u
+                  : 0x12ab65u;
+}
+
+// Montgomery product a * b * 2^-261 mod r (lazy: output < 3.3 r for inputs
+// < 32 r).  FIPS, one 64-bit accumulator; -r^-1 mod 2^29 = 2^29 - 1, so the
+// quotient digit is m = -t mod 2^29, and m * r[0] = m clears the low digit.
+__device__ __forceinline__ F29 f29_mul(const F29& a, const F29& b) {
+    uint32_t m[9];
+    F29 o;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+#pragma unroll
+        for (int j = 0; j < k; ++j) {
+            acc += (uint64_t)a.l[j] * b.l[k - j];
+            acc += (uint64_t)m[j] * p29(k - j);
+        }
+        acc += (uint64_t)a.l[k] * b.l[0];
+        m[k] = (0u - (uint32_t)acc) & F29_MASK;
+        acc = (acc + m[k]) >> 29;
+    }
+#pragma unroll
+    for (int k = 9; k < 17; ++k) {
+#pragma unroll
+        for (int j = k - 8; j < 9; ++j) {
+            acc += (uint64_t)a.l[j] * b.l[k - j];
+            acc += (uint64_t)m[j] * p29(k - j);
+        }
+        o.l[k - 9] = (uint32_t)acc & F29_MASK;
+        acc >>= 29;
+    }
+    o.l[8] = (uint32_t)acc;
+    return o;
+}
+
+// Montgomery square: cross products a_i a_j (i < j) taken once against the
+// doubled limb 2 a_i (< 2^30, products < 2^59): 45 + 72 products instead of
+// 81 + 72.  Column bound: <= 5 such products + 8 m*r products + carry < 2^62.
+__device__ __forceinline__ F29 f29_sqr(const F29& a) {
+    uint32_t m[9], d[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) d[i] = a.l[i] << 1;
+    F29 o;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+#pragma unroll
+        for (int i = (k > 8 ? k - 8 : 0); 2 * i < k; ++i) acc += (uint64_t)d[i] * a.l[k - i];
+        if ((k & 1) == 0) acc += (uint64_t)a.l[k / 2] * a.l[k / 2];
+#pragma unroll
+        for (int j = (k > 8 ? k - 8 : 0); j < (k < 9 ? k : 9); ++j) acc += (uint64_t)m[j] * p29(k - j);
+        if (k < 9) {
+            m[k] = (0u - (uint32_t)acc) & F29_MASK;
+            acc = (acc + m[k]) >> 29;
+        } else {
+            o.l[k - 9] = (uint32_t)acc & F29_MASK;
+            acc >>= 29;
+        }
+    }
+    o.l[8] = (uint32_t)acc;
+    return o;
+}
+
+// limb-wise sum + carry propagation (no modular reduction)
+__device__ __forceinline__ F29 f29_add(const F29& a, const F29& b) {
+    F29 o;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t s = a.l[i] + b.l[i] + c;
+        o.l[i] = s & F29_MASK;
+        c = s >> 29;
+    }
+    o.l[8] = a.l[8] + b.l[8] + c;
+    return o;
+}
+
+// value - q*r for the small q estimated from the top limb, so that the result
+// is < 2r for any input < 2^261 (q_est <= floor(v / r) <= q_est + 1)
+__device__ __forceinline__ F29 f29_reduce(const F29& a) {
+    // r / 2^232 = 1223525.37; q = floor(l8 / 1223526) never exceeds floor(v / r)
+    // and leaves v - q r < 2r (checked exhaustively over l8 in tests/ubench)
+    const uint32_t q = (uint32_t)(((uint64_t)a.l[8] * 0xdb651d12ull) >> 52);
+    F29 o;
+    int64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int64_t s = (int64_t)a.l[i] - (int64_t)q * p29(i) + c;
+        o.l[i] = (uint32_t)s & F29_MASK;
+        c = s >> 29;  // arithmetic shift: signed carry
+    }
+    o.l[8] = (uint32_t)((int64_t)a.l[8] - (int64_t)q * p29(8) + c);
+    return o;
+}
+
+// x < 2^256 as 8 x 32-bit words -> 9 x 29-bit limbs (same integer)
+__device__ __forceinline__ F29 f29_repack_in(const Fr& x) {
+    F29 o;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const int bit = 29 * i, w = bit >> 5, s = bit & 31;
+        uint64_t v = x.v[w];
+        if (w + 1 < 8) v |= (uint64_t)x.v[w + 1] << 32;
+        o.l[i] = (uint32_t)(v >> s) & (i < 8 ? F29_MASK : 0xffffffffu);
+    }
+    return o;
+}
+
+__device__ __forceinline__ Fr f29_repack_out(const F29& a) {
+    Fr o;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const int bit = 32 * w;
+        const int i = bit / 29, s = bit % 29;
+        uint64_t v = (uint64_t)a.l[i] >> s;
+        if (i + 1 < 9) v |= (uint64_t)a.l[i + 1] << (29 - s);
+        if (i + 2 < 9) v |= (uint64_t)a.l[i + 2] << (58 - s);
+        o.v[w] = (uint32_t)v;
+    }
+    return o;
+}
+
+__device__ __forceinline__ F29 f29_const(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3, uint32_t l4, uint32_t l5,
+                                         uint32_t l6, uint32_t l7, uint32_t l8) {
+    F29 o;
+    o.l[0] = l0; o.l[1] = l1; o.l[2] = l2; o.l[3] = l3; o.l[4] = l4;
+    o.l[5] = l5; o.l[6] = l6; o.l[7] = l7; o.l[8] = l8;
+    return o;
+}
+
+// ark-ff Montgomery (x 2^256) -> F29 (x 2^261): times 2^5 via a product by 2^266 mod r
+__device__ __forceinline__ F29 f29_from_fr(const Fr& x) {
+    const F29 c = f29_const(0x1fffc927u, 0x1153ffffu, 0x1ff1bfb1u, 0xec4435fu, 0x185f1096u, 0x1ce80ad5u,
+                            0x587fb98u, 0x93ca8f4u, 0x5551eu);
+    return f29_mul(f29_repack_in(x), c);
+}
+
+// F29 -> canonical ark-ff Montgomery words: times 2^-5 (product by 2^256 mod r), reduce to [0, r)
+__device__ __forceinline__ Fr f29_to_fr(const F29& x) {
+    const F29 c = f29_const(0x1ffffff3u, 0x8e3ffffu, 0x1ffffc9fu, 0xfea1edfu, 0xfee725u, 0xabaa896u, 0xa745b60u,
+                            0x6457773u, 0xd4bdau);
+    F29 y = f29_mul(f29_reduce(x), c);  // < 3.3 r
+    Fr o = f29_repack_out(y);           // < 4r < 2^256
+    o = fr_reduce_once(o);
+    o = fr_reduce_once(o);
+    return fr_reduce_once(o);
+}
+
+}  // namespace lsp

@@ -153,7 +153,8 @@ struct lsp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     lsp::P2Host p2;
-    lsp::Fr* rc_dev = nullptr;
+    lsp::Fr* rc_dev = nullptr;    // round constants, ark form
+    lsp::F29* rc29_dev = nullptr; // the same in the 29-bit-limb form the hash kernels use
     uint32_t log_blowup = 3, log_final_poly_len = 0, num_queries = 33, pow_bits = 0;
     int32_t public_degree = 1;
     std::string err;

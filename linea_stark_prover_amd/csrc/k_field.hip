@@ -31,18 +31,20 @@ __global__ __launch_bounds__(256) void k_batch_inverse(const Fr* __restrict__ in
     }
 }
 
-// Fr-mul throughput probe: 4 independent register-resident chains per lane
+// Fr-mul throughput probe of the multiplier the Poseidon2 kernels use (the
+// 29-bit-limb product, fr29.hpp): 4 independent register-resident chains per lane
 __global__ __launch_bounds__(256) void k_calib_mul(Fr* __restrict__ out, uint32_t iters) {
     const size_t t = gtid();
-    Fr a = fr_from_u64(t + 3), b = fr_from_u64(t * 7 + 5), c = fr_from_u64(t + 11), d = fr_from_u64(t + 13);
-    const Fr m = fr_from_u64(0x1234567u + (uint32_t)t);
+    F29 a = f29_from_fr(fr_from_u64(t + 3)), b = f29_from_fr(fr_from_u64(t * 7 + 5)),
+        c = f29_from_fr(fr_from_u64(t + 11)), d = f29_from_fr(fr_from_u64(t + 13));
+    const F29 m = f29_from_fr(fr_from_u64(0x1234567u + (uint32_t)t));
     for (uint32_t i = 0; i < iters; ++i) {
-        a = fr_mul(a, m);
-        b = fr_mul(b, m);
-        c = fr_mul(c, m);
-        d = fr_mul(d, m);
+        a = f29_mul(a, m);
+        b = f29_mul(b, m);
+        c = f29_mul(c, m);
+        d = f29_mul(d, m);
     }
-    out[t] = fr_add(fr_add(a, b), fr_add(c, d));
+    out[t] = fr_add(fr_add(f29_to_fr(a), f29_to_fr(b)), fr_add(f29_to_fr(c), f29_to_fr(d)));
 }
 
 __global__ __launch_bounds__(256) void k_gather(const uint64_t* __restrict__ ptrs, Fr* __restrict__ out, size_t n) {

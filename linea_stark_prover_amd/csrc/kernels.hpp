@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "fr.hpp"
+#include "fr29.hpp"
 #include "poseidon2.hpp"
 
 namespace lsp {
@@ -36,13 +37,15 @@ struct MatList {
     uint32_t width[8];
     uint32_t n;
 };
-hipError_t launch_permute(Fr* states, size_t n, const Fr* rc, P2Layout L, hipStream_t st);
+// round constants (ark form) -> the 29-bit-limb form the permutation kernels take
+hipError_t launch_rc_to_f29(const Fr* rc, F29* rc29, uint32_t n, hipStream_t st);
+hipError_t launch_permute(Fr* states, size_t n, const F29* rc29, P2Layout L, hipStream_t st);
 // out[i] = hash_iter(concat of row i of every matrix in `m`)
-hipError_t launch_hash_rows(const MatList& m, size_t nrows, Fr* out, const Fr* rc, P2Layout L, hipStream_t st);
+hipError_t launch_hash_rows(const MatList& m, size_t nrows, Fr* out, const F29* rc29, P2Layout L, hipStream_t st);
 // dst[i] = compress(src[2i], src[2i+1]) for i < nout
-hipError_t launch_merkle_level(const Fr* src, Fr* dst, size_t nout, const Fr* rc, P2Layout L, hipStream_t st);
+hipError_t launch_merkle_level(const Fr* src, Fr* dst, size_t nout, const F29* rc29, P2Layout L, hipStream_t st);
 // full tree above the leaf digests already stored at layers[0..nleaves)
-hipError_t launch_merkle_tree(Fr* layers, size_t nleaves, const Fr* rc, P2Layout L, hipStream_t st);
+hipError_t launch_merkle_tree(Fr* layers, size_t nleaves, const F29* rc29, P2Layout L, hipStream_t st);
 
 // --------------------------------------------------------- k_field.hip
 // out[i] = 1 / in[i] (Montgomery trick, interleaved chunks); in may alias out? no

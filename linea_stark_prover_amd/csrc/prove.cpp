@@ -118,8 +118,8 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
 
 // ------------------------------------------------------------- Merkle
 Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers) {
-    LSP_HIP(launch_hash_rows(m, height, layers, ctx->rc_dev, ctx->p2.L, ctx->stream));
-    LSP_HIP(launch_merkle_tree(layers, height, ctx->rc_dev, ctx->p2.L, ctx->stream));
+    LSP_HIP(launch_hash_rows(m, height, layers, ctx->rc29_dev, ctx->p2.L, ctx->stream));
+    LSP_HIP(launch_merkle_tree(layers, height, ctx->rc29_dev, ctx->p2.L, ctx->stream));
     return d2h_fr(ctx, layers + 2 * height - 2);
 }
 

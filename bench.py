@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-n", type=int, default=19)
     ap.add_argument("--ncols", type=int, default=3)
+    ap.add_argument("--air", choices=["perm", "wide"], default="perm",
+                    help="perm: the 3x3 permutation AIR (headline); wide: SURVEY 8(d) C3 synthetic "
+                         "wide AIR (4 LogUp lookups + 8 permutation groups of 6+6, W = 184)")
     ap.add_argument("--seed", type=int, default=0x4C494E4541)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-log-n", type=int, default=17, help="bounded CPU-baseline sample size")
@@ -58,16 +61,19 @@ def main():
     import numpy as np
 
     from linea_stark_prover_amd.air import permutation_air
-    from linea_stark_prover_amd.prover import Context, StarkConfig, gen_permutation_trace
+    from linea_stark_prover_amd.prover import Context, StarkConfig, gen_permutation_trace, gen_wide_trace
 
     cfg = StarkConfig(seed=args.seed)
     ctx = Context(cfg, device=local)
     a, d, _ = cfg.seeded()
     pub = np.concatenate([a, d])
-    air = permutation_air(args.ncols)
     h = 1 << args.log_n
-    w = 2 * args.ncols + 2
-    trace = gen_permutation_trace(args.log_n, args.ncols, a, d, seed=rank_seed(args.seed, rank))
+    if args.air == "wide":
+        trace, air = gen_wide_trace(args.log_n, a, d, seed=rank_seed(args.seed, rank))
+    else:
+        air = permutation_air(args.ncols)
+        trace = gen_permutation_trace(args.log_n, args.ncols, a, d, seed=rank_seed(args.seed, rank))
+    w = trace.shape[1]
     dtrace = ctx.dev_alloc(trace.nbytes)
     ctx.h2d(dtrace, trace)  # resident in HBM before the timed region
 
@@ -86,7 +92,12 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         value = world * h * args.steps / elapsed
         N = h << cfg.log_blowup
-        q = 4 if args.ncols <= 3 else 8
+        import ctypes
+        from linea_stark_prover_amd import _lib
+        desc = (ctypes.c_int32 * len(air.descriptor()))(*air.descriptor())
+        lq = ctypes.c_uint32()
+        _lib.check(_lib.lib().lsp_log_quotient_degree(desc, len(desc), cfg.public_degree, ctypes.byref(lq)))
+        q = 1 << lq.value
         lde_ms = phases.get("coset_lde_batch", float("nan"))
         lde_bytes = 32 * w * (h + N)
         achieved = lde_bytes / (lde_ms * 1e-3) / 1e9
@@ -117,28 +128,45 @@ def main():
                                    "source": "reference README.md:11, ~330 s for 2^19 rows on a 16-core CPU"},
             "dtype": "fr253 (BLS12-377 Fr, 8x u32 Montgomery limbs)",
             "data": "synthetic (seeded permutation trace, SURVEY 8(d) C1)",
-            "config": {"workload": f"{args.ncols}x{args.ncols} permutation AIR, 2^{args.log_n} rows "
-                                   f"(w={w}, q={q} quotient chunks, log_blowup {cfg.log_blowup}, "
-                                   f"{cfg.num_queries} queries, Poseidon2-w3 Merkle, FRI)",
+            "config": {"workload": (f"{args.ncols}x{args.ncols} permutation AIR" if args.air == "perm" else
+                                    "wide AIR (4 LogUp lookups + 8 permutation groups of 6+6)") +
+                                   f", 2^{args.log_n} rows (w={w}, q={q} quotient chunks, log_blowup "
+                                   f"{cfg.log_blowup}, {cfg.num_queries} queries, Poseidon2-w3 Merkle, FRI)",
                        "log_n": args.log_n, "width": w, "fri_queries": cfg.num_queries,
                        "parallelism": "replicas" if world > 1 else "single-gpu"},
             "verified": bool(verified),
             "phases_ms": {k: round(v, 3) for k, v in phases.items()},
             "roofline": {"bound": "hbm", "kernel": "coset_lde_batch (trace, w x 2^log_n -> 8x)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": lde_traffic(args.log_n, w),
                          "algorithmic_bytes": lde_bytes, "ms": lde_ms},
             "roofline_valu": {"bound": "valu", "kernel": "trace Merkle tree (Poseidon2 leaf hash + levels)",
                               "achieved": valu_achieved, "unit": "G Fr-mul/s",
                               "peak": calib, "frac": (valu_achieved / calib) if calib else None,
                               "perms": trace_perms, "mul_per_perm": mul_per_perm, "ms": merkle_ms},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.air == "perm":
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     ctx.dev_free(dtrace)
     ctx.close()
     dist.close()
+
+
+def lde_traffic(log_n, w):
+    """HBM bytes per coset_lde_batch from the rocprofv3 PMC passes of
+    tools/pmc_round.sh (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), kept in
+    profiles/; None when no measurement matches this size."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_lde_traffic.json"))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("h") == (1 << log_n) and d.get("w") == w:
+            best = d["traffic_bytes"]
+    return best
 
 
 def cpu_baseline(args):

@@ -201,6 +201,17 @@ int lsp_calibrate_fr_mul(lsp_ctx *ctx, double *gmul_per_s);
 int lsp_gen_permutation_trace(uint64_t seed, uint32_t log_n, uint32_t ncols, const lsp_fr *alpha,
                               const lsp_fr *delta, int small_values, lsp_fr *rows_out);
 
+/* Synthetic wide trace (stand-in for the missing zkevm.bin):
+ * nlookup LogUp lookups (RawLookupTrace::get_trace, trace/src/lookup.rs:46-176;
+ * A = na columns drawn from ntab tables of na columns) then nperm permutation
+ * groups of pcols + pcols columns, laid out as RawTrace::push_traces does
+ * (trace/src/lib.rs:62-106).  Call with rows_out == NULL to get the width and
+ * the AIR descriptor length; then with buffers of h*width elements and
+ * air_len int32s. */
+int lsp_gen_wide_trace(uint64_t seed, uint32_t log_n, uint32_t nlookup, uint32_t na, uint32_t ntab, uint32_t nperm,
+                       uint32_t pcols, const lsp_fr *alpha, const lsp_fr *delta, lsp_fr *rows_out, size_t rows_cap,
+                       int32_t *air_out, size_t air_cap, size_t *width_out, size_t *air_len_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -86,6 +86,34 @@ class LineaAIR:
             out += c.encode()
         return out
 
+    @staticmethod
+    def from_descriptor(d: List[int]) -> "LineaAIR":
+        it = iter(d)
+        n = next(it)
+        cfgs: List[AirConfig] = []
+        for _ in range(n):
+            t = next(it)
+            if t == LSP_AIR_PERMUTATION:
+                na, nb = next(it), next(it)
+                a = [next(it) for _ in range(na)]
+                b = [next(it) for _ in range(nb)]
+                cfgs.append(AirPermutationConfig(a, b, next(it), next(it)))
+            elif t == LSP_AIR_LOOKUP:
+                na = next(it)
+                a = [next(it) for _ in range(na)]
+                nt, nbc = next(it), next(it)
+                b = [[next(it) for _ in range(nbc)] for _ in range(nt)]
+                af = next(it)
+                bf = [next(it) for _ in range(nt)]
+                ai = next(it)
+                bi = [next(it) for _ in range(nt)]
+                oc = [next(it) for _ in range(nt)]
+                cfgs.append(AirLookupConfig(a, b, af, bf, ai, bi, oc, next(it)))
+            else:
+                raise ValueError(f"unknown AIR config type {t}")
+        assert next(it, None) is None, "trailing data in AIR descriptor"
+        return LineaAIR(cfgs)
+
 
 def permutation_air(ncols: int) -> LineaAIR:
     """The benchmark AIR: one permutation group of ncols 'from' + ncols 'to'

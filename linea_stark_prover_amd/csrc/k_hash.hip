@@ -87,6 +87,29 @@ __global__ __launch_bounds__(64) void k_merkle_top(Fr* __restrict__ layers, size
         len = nout;
     }
 }
+// PoW grinding (GrindingChallenger::grind, [EXT p3-challenger]; U8): each lane
+// tests candidate witnesses w: the sponge state before the block holding w is
+// fixed (host), w is absorbed into lane `wlane` (the other rate lane keeps
+// `other`), one permutation, then the low `bits` of the canonical s0 must be 0.
+// The smallest hit of the batch is kept with an atomic min.
+template <uint32_t D>
+__global__ __launch_bounds__(256) void k_grind(Fr pre0, Fr pre1, Fr pre2, uint32_t wlane, uint64_t base,
+                                               uint64_t count, uint32_t bits, const F29* __restrict__ rc,
+                                               uint32_t rf, uint32_t rp, unsigned long long* __restrict__ best) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const F29 c0 = f29_from_fr(pre0), c1 = f29_from_fr(pre1), c2 = f29_from_fr(pre2);
+    const uint64_t mask = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
+    for (uint64_t i = gtid(); i < count; i += stride) {
+        const uint64_t w = base + i;
+        const F29 fw = f29_from_fr(fr_from_u64(w));
+        F29 s0 = wlane == 0 ? fw : c0, s1 = wlane == 0 ? c1 : fw, s2 = c2;
+        permute3_f29<D>(s0, s1, s2, rc, rf, rp);
+        const Fr c = fr_to_canonical(f29_to_fr(s0));
+        const uint64_t lo = (uint64_t)c.v[0] | ((uint64_t)c.v[1] << 32);
+        if ((lo & mask) == 0) atomicMin(best, (unsigned long long)w);
+    }
+}
+
 __global__ void k_rc_to_f29(const Fr* __restrict__ rc, F29* __restrict__ rc29, uint32_t n) {
     const uint32_t i = (uint32_t)gtid();
     if (i < n) rc29[i] = f29_from_fr(rc[i]);
@@ -121,6 +144,14 @@ hipError_t launch_hash_rows(const MatList& m, size_t nrows, Fr* out, const F29* 
     else
         LSP_DISPATCH_D(L, k_hash_rows_multi, dim3(nblocks(nrows, bs)), dim3(bs), 0, st, m, nrows, out, rc,
                        L.rounds_f, L.rounds_p);
+    return hipGetLastError();
+}
+
+hipError_t launch_grind(const Fr pre[3], uint32_t wlane, uint64_t base, uint64_t count, uint32_t bits,
+                        const F29* rc, P2Layout L, unsigned long long* best, hipStream_t st) {
+    const unsigned blocks = 256 * 16;
+    LSP_DISPATCH_D(L, k_grind, dim3(blocks), dim3(256), 0, st, pre[0], pre[1], pre[2], wlane, base, count, bits, rc,
+                   L.rounds_f, L.rounds_p, best);
     return hipGetLastError();
 }
 

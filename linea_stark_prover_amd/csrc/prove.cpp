@@ -136,6 +136,55 @@ static void tree_path(const std::vector<Fr>& got, size_t& cur, uint32_t lg, std:
     cur += lg;
 }
 
+// --------------------------------------------------------------- grind
+// GrindingChallenger::grind(bits) on the device: the smallest witness w >= 0
+// with sample_bits(bits) == 0 after observe(w) (U8).  The sponge over the
+// challenger's input buffer is absorbed on the host up to the block that
+// will hold w; the device runs the last permutation for 2^22 candidates per
+// launch.  The winner is re-checked on the host transcript.
+uint64_t grind_device(lsp_ctx* ctx, Challenger& ch, uint32_t bits) {
+    if (bits == 0) {
+        LSP_REQUIRE(ch.check_witness(0, 0), LSP_E_STATE, "grind(0) must accept w = 0");
+        return 0;
+    }
+    const std::vector<Fr>& in = ch.in;  // observe(w) clears the output buffer and appends w
+    Fr s0 = fr_zero(), s1 = fr_zero(), s2 = fr_zero();
+    size_t k = 0;
+    while (k + 2 <= in.size()) {
+        s0 = in[k];
+        s1 = in[k + 1];
+        ctx->p2.permute(s0, s1, s2);
+        k += 2;
+    }
+    uint32_t wlane;
+    Fr pre[3];
+    if (k < in.size()) {  // odd prefix: [last, w] form the final block
+        pre[0] = in[k];
+        pre[1] = s1;
+        pre[2] = s2;
+        wlane = 1;
+    } else {  // even prefix: w alone in lane 0, lane 1 keeps the previous state
+        pre[0] = s0;
+        pre[1] = s1;
+        pre[2] = s2;
+        wlane = 0;
+    }
+    unsigned long long* best = (unsigned long long*)ctx->buf("grind_best", sizeof(unsigned long long));
+    const uint64_t batch = 1ull << 22;
+    for (uint64_t base = 0;; base += batch) {
+        LSP_HIP(hipMemsetAsync(best, 0xff, sizeof(unsigned long long), ctx->stream));
+        LSP_HIP(launch_grind(pre, wlane, base, batch, bits, ctx->rc29_dev, ctx->p2.L, best, ctx->stream));
+        unsigned long long got = 0;
+        LSP_HIP(hipMemcpyAsync(&got, best, sizeof(got), hipMemcpyDeviceToHost, ctx->stream));
+        LSP_HIP(hipStreamSynchronize(ctx->stream));
+        if (got != ~0ull) {
+            LSP_REQUIRE(ch.check_witness(bits, got), LSP_E_STATE, "device grind witness rejected by the transcript");
+            return got;
+        }
+        LSP_REQUIRE(base < (1ull << 50), LSP_E_STATE, "grinding did not terminate");
+    }
+}
+
 // ------------------------------------------------------------- prove
 lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, const Air& air, const Fr* pub,
                         size_t npub) {
@@ -375,7 +424,7 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
             for (const Fr& c : proof->final_poly) ch.observe(c);
         }
         T.begin("grind for proof-of-work witness");
-        proof->pow_w = fr_from_u64(ch.grind(ctx->pow_bits));
+        proof->pow_w = fr_from_u64(grind_device(ctx, ch, ctx->pow_bits));
         T.end("grind for proof-of-work witness");
 
         // ---- query phase: one gather for every opened element

@@ -314,6 +314,21 @@ def gen_permutation_trace(log_n: int, ncols: int, alpha: np.ndarray, delta: np.n
     return out
 
 
+def gen_wide_trace(log_n: int, alpha: np.ndarray, delta: np.ndarray, nlookup: int = 4, na: int = 3, ntab: int = 2,
+                   nperm: int = 8, pcols: int = 6, seed: int = DEFAULT_SEED) -> Tuple[np.ndarray, LineaAIR]:
+    """SURVEY 8(d) C3 wide AIR (default: 4 LogUp lookups with 3-column A and two
+    3-column tables, 8 permutation groups of 6+6; width 184).  Returns the
+    (2^log_n, W, 4) trace and its LineaAIR."""
+    w, dl = ctypes.c_size_t(), ctypes.c_size_t()
+    args = (seed, log_n, nlookup, na, ntab, nperm, pcols, _ptr(_fr_arr(alpha)), _ptr(_fr_arr(delta)))
+    L.check(L.lib().lsp_gen_wide_trace(*args, None, 0, None, 0, ctypes.byref(w), ctypes.byref(dl)))
+    rows = np.zeros((1 << log_n, w.value, 4), np.uint64)
+    desc = (ctypes.c_int32 * dl.value)()
+    L.check(L.lib().lsp_gen_wide_trace(*args, _ptr(rows), rows.shape[0] * w.value, desc, dl.value, ctypes.byref(w),
+                                       ctypes.byref(dl)))
+    return rows, LineaAIR.from_descriptor(list(desc))
+
+
 def prove(config: StarkConfig, air: LineaAIR, trace: np.ndarray, public_values: np.ndarray,
           ctx: Optional[Context] = None) -> bytes:
     """p3_uni_stark::prove(&config, &air, &mut challenger, trace, &public_values)."""
@@ -338,4 +353,4 @@ def verify(config: StarkConfig, air: LineaAIR, proof: bytes, public_values: np.n
 
 
 __all__ = ["StarkConfig", "Context", "Radix2DitParallel", "MerkleTreeMmcs", "MerkleTree",
-           "TwoAdicFriGenericConfig", "gen_permutation_trace", "prove", "verify", "to_mont"]
+           "TwoAdicFriGenericConfig", "gen_permutation_trace", "gen_wide_trace", "prove", "verify", "to_mont"]

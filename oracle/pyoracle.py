@@ -593,6 +593,38 @@ def synthetic_perm_trace(log_n: int, ncols: int, alpha: int, delta: int, seed: i
     return [cfg], cols
 
 
+def synthetic_wide_trace(log_n: int, alpha: int, delta: int, seed: int, nlookup=4, na=3, ntab=2, nperm=8,
+                         pcols=6):
+    """SURVEY 8(d) C3 wide AIR: nlookup LogUp lookups (A rows drawn from ntab
+    random tables), then nperm permutation groups; RawTrace push order
+    (trace/src/lib.rs:81-89: lookups first).  Returns (cfgs, columns)."""
+    n = 1 << log_n
+    rng = SplitMix64(seed ^ 0x57494445)  # "WIDE"
+    cols, cfgs = [], []
+    for _ in range(nlookup):
+        b = [[[rng.sample_fr() for _ in range(n)] for _ in range(na)] for _ in range(ntab)]
+        a = [[0] * n for _ in range(na)]
+        for i in range(n):
+            t = rng.below(ntab)
+            j = rng.below(n)
+            for c in range(na):
+                a[c][i] = b[t][c][j]
+        cfg, lc = lookup_witness(a, b, [1] * n, [[1] * n for _ in range(ntab)], alpha, delta)
+        cfgs.append(shift_cfg(cfg, len(cols)))
+        cols += lc
+    for _ in range(nperm):
+        a = [[rng.sample_fr() for _ in range(n)] for _ in range(pcols)]
+        perm = list(range(n))
+        for i in range(n - 1, 0, -1):
+            j = rng.below(i + 1)
+            perm[i], perm[j] = perm[j], perm[i]
+        b = [[col[perm[i]] for i in range(n)] for col in a]
+        cfg, pc = perm_witness(a, b, alpha, delta)
+        cfgs.append(shift_cfg(cfg, len(cols)))
+        cols += pc
+    return cfgs, cols
+
+
 # ---------------------------------------------------------------------------
 # A9 -- selectors_on_coset; A10 -- quotient_values; A11 -- split_evals
 # ---------------------------------------------------------------------------

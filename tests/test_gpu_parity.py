@@ -293,3 +293,19 @@ def test_prove_large_self_consistency(gpu_ctx):
     pf2 = gpu_ctx.prove(tr, air, pub)
     assert pf1 == pf2
     assert gpu_ctx.verify(pf1, air, pub)
+
+
+@pytest.mark.parametrize("bits", [1, 8, 13])
+def test_prove_with_pow_grinding_matches_oracle(oracle_lib, bits):
+    """F2: GPU grinding finds the same (smallest) witness as the oracle."""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import Context, StarkConfig
+    s, p, trace, w = _perm_setup(5, 3, oracle_lib)
+    cfg = StarkConfig(proof_of_work_bits=bits)
+    with Context(cfg) as ctx:
+        got = ctx.prove(trace, permutation_air(3), _pub(p))
+        assert ctx.verify(got, permutation_air(3), _pub(p))
+    fri = oracle_lib.fri_params(O.FriParams(proof_of_work_bits=bits))
+    exp = oracle_lib.prove(p, trace.ctypes.data, 32, w, oracle_lib.perm_air(3), fri=fri)
+    assert got == exp
+    assert oracle_lib.verify(p, got, oracle_lib.perm_air(3), fri=fri) == 0

@@ -1,0 +1,19 @@
+"""GPU parity on the wide AIR (LogUp lookups + permutation groups): the
+quotient interpreter over many configs, wide rows in the leaf hash."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("log_n,shape", [(4, (4, 3, 2, 8, 6)), (7, (2, 3, 2, 3, 6)), (9, (1, 3, 2, 1, 3))])
+def test_wide_prove_matches_oracle(gpu_ctx, oracle_lib, log_n, shape):
+    from linea_stark_prover_amd.prover import gen_wide_trace
+    a, d, _ = gpu_ctx.config.seeded()
+    tr, air = gen_wide_trace(log_n, a, d, *shape)
+    pub = np.concatenate([a, d])
+    got = gpu_ctx.prove(tr, air, pub)
+    assert gpu_ctx.verify(got, air, pub)
+    p = oracle_lib.setup()
+    exp = oracle_lib.prove(p, tr.ctypes.data, 1 << log_n, tr.shape[1], air.descriptor())
+    assert got == exp

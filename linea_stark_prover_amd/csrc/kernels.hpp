@@ -12,24 +12,20 @@
 namespace lsp {
 
 // ------------------------------------------------------------ k_ntt.hip
-// dst[b][c][r] = src[b][rp(r)][c]; src is batch x R x C row-major,
-// rp = bit reversal over log2(R) bits when bitrev_rows, identity otherwise.
-hipError_t launch_transpose(const Fr* src, Fr* dst, size_t batch, size_t R, size_t C, bool bitrev_rows,
-                            hipStream_t st);
-// In-place radix-2 NTT over `batch` contiguous arrays of 2^logH elements.
-// dif=true : natural in -> bit-reversed out, twiddles tw[x] = w^x (x < H/2)
-// dif=false: bit-reversed in -> natural out (DIT)
-hipError_t launch_ntt(Fr* data, size_t batch, uint32_t logH, const Fr* tw, bool dif, hipStream_t st);
+// Bit-reversed coset LDE of the h x w row-major matrix `in` into the
+// (h << added_bits) x w row-major `out` (block k = coset k), via X (h x w
+// scratch, left holding h * coefficients).  tw_inv / tw_fwd: w_h^-x / w_h^x,
+// x < h/2.  twist: two-level tables (L1, L2) of base s and scale 1/h, one per
+// coset (twist_per_col = 0) or per (coset, column) at index k*w + c.
+hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t added_bits, const Fr* tw_inv,
+                      const Fr* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
+                      hipStream_t st);
 // Two-level power tables: for each base b,
 // tab[b] = {b^j, j < 2^L1} ++ {b^(j 2^L1) * scale[b], j < 2^L2}   (scale nullable)
 hipError_t launch_pow_tables(const Fr* bases, size_t nbases, uint32_t L1, uint32_t L2, const Fr* scale,
                              Fr* tabs, hipStream_t st);
 // out[i] = base^i for i < n, from a two-level table of base
 hipError_t launch_powers(const Fr* tab, uint32_t L1, size_t n, Fr* out, hipStream_t st);
-// Y[(k*w + c)*h + i] = X[c*h + i] * pow2l(tab_{k*w+c}, i); the inverse transform's
-// 1/h is folded into the tables' scale
-hipError_t launch_twist_expand(const Fr* X, Fr* Y, size_t w, uint32_t logh, uint32_t ncosets, const Fr* tabs,
-                               uint32_t L1, uint32_t L2, hipStream_t st);
 
 // ----------------------------------------------------------- k_hash.hip
 struct MatList {

@@ -86,18 +86,17 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
     const uint32_t logN = logh + added_bits;
     LSP_REQUIRE(logN <= 47, LSP_E_SIZE, "LDE larger than the 2-adic subgroup");
     Fr* X = ctx->fbuf("lde_X", h * w);
-    Fr* Y = ctx->fbuf("lde_Y", h * w * B);
     hipStream_t st = ctx->stream;
-    // X[c][j] = in[bitrev(j)][c]  (bit-reversed input of the DIT inverse)
-    LSP_HIP(launch_transpose(d_in, X, 1, h, w, true, st));
-    LSP_HIP(launch_ntt(X, w, logh, ctx->twiddle(logh, true), false, st));  // X = h * coefficients
-    // coset k, column c: base s = shift_c * w_N^bitrev_B(k); Y = X * s^i / h
+    // coset k, column c: base s = shift_c * w_N^bitrev_B(k); coefficient i is scaled by s^i / h
+    bool shared = true;
+    for (size_t c = 1; c < w; ++c) shared = shared && fr_eq(shifts_host[c], shifts_host[0]);
+    const size_t per_coset = shared ? 1 : w;
     const Fr wN = host_two_adic_generator(logN);
     const Fr hinv = fr_inv(fr_from_u64(h));
-    std::vector<Fr> bases((size_t)B * w), scales((size_t)B * w, hinv);
+    std::vector<Fr> bases((size_t)B * per_coset), scales((size_t)B * per_coset, hinv);
     for (uint32_t k = 0; k < B; ++k) {
         const Fr ck = fr_pow_u64(wN, host_bitrev(k, added_bits));
-        for (size_t c = 0; c < w; ++c) bases[k * w + c] = fr_mul(shifts_host[c], ck);
+        for (size_t c = 0; c < per_coset; ++c) bases[k * per_coset + c] = fr_mul(shifts_host[c], ck);
     }
     uint32_t L1, L2;
     two_level(logh, L1, L2);
@@ -108,10 +107,8 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
     const size_t per = (1ull << L1) + (1ull << L2);
     Fr* tabs = ctx->fbuf("lde_tabs", per * bases.size());
     LSP_HIP(launch_pow_tables(dbases, bases.size(), L1, L2, dbases + bases.size(), tabs, st));
-    LSP_HIP(launch_twist_expand(X, Y, w, logh, B, tabs, L1, L2, st));
-    LSP_HIP(launch_ntt(Y, (size_t)B * w, logh, ctx->twiddle(logh, false), true, st));
-    // out block k = transpose of Y_k (w x h) -> h x w
-    LSP_HIP(launch_transpose(Y, d_out, B, w, h, false, st));
+    LSP_HIP(launch_lde(d_in, X, d_out, w, logh, added_bits, ctx->twiddle(logh, true), ctx->twiddle(logh, false), tabs,
+                       L1, L2, shared ? 0 : 1, st));
     // host vectors (bases, scales) must outlive the async copies
     LSP_HIP(hipStreamSynchronize(st));
 }

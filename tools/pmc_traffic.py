@@ -14,9 +14,17 @@ def per_dispatch(path):
     return out
 
 def calls(d):
-    """group dispatches into LDE calls: each call starts and ends with k_transpose"""
-    ts = [k for k in sorted(d) if 'k_transpose' in d[k][0]]
-    return [(ts[i], ts[i + 1]) for i in range(0, len(ts) - 1, 2)]
+    """group dispatches into LDE calls: a call is its twist-table kernel (k_pow_tables)
+    followed by the NTT passes (k_ntt_rm), up to the next call"""
+    ks = sorted(d)
+    starts = [k for k in ks if 'k_pow_tables' in d[k][0]]
+    out = []
+    for i, s in enumerate(starts):
+        end = starts[i + 1] if i + 1 < len(starts) else ks[-1] + 1
+        body = [k for k in ks if s <= k < end and 'copyBuffer' not in d[k][0]]
+        if any('k_ntt_rm' in d[k][0] for k in body):
+            out.append((body[0], body[-1]))
+    return out
 
 fetch = per_dispatch(sys.argv[1]); write = per_dispatch(sys.argv[2])
 h, w, added = int(sys.argv[3]), int(sys.argv[4]), 3
@@ -25,10 +33,10 @@ kern = [k for k in sorted(fetch) if lo <= k <= hi and 'copyBuffer' not in fetch[
 fb = sum(fetch[k][1] for k in kern) * 1024 * 2
 wb = sum(write[k][1] for k in kern if k in write) * 1024
 alg = 32 * w * (h + (h << added))
-res = {"kernel": "coset_lde_batch (transpose, 3 DIT passes, twist, 3 DIF passes, transpose)",
+res = {"kernel": "coset_lde_batch (twist tables, 3 row-major DIT passes, 3 row-major DIF passes with fused twist)",
        "h": h, "w": w, "fetch_bytes": fb, "write_bytes": wb, "traffic_bytes": fb + wb,
        "algorithmic_bytes": alg, "traffic_over_algorithmic": (fb + wb) / alg,
-       "per_kernel": [{"dispatch": k, "kernel": fetch[k][0].split('(')[0].replace('lsp::(anonymous namespace)::', ''),
+       "per_kernel": [{"dispatch": k, "kernel": fetch[k][0].replace('lsp::(anonymous namespace)::', '').replace('void ', '').split('(')[0],
                        "fetch_bytes_x2": fetch[k][1] * 2048, "write_bytes": write.get(k, [0, 0])[1] * 1024}
                       for k in kern],
        "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE separate passes on tools/lde_probe.py; FETCH x2 (gfx950)"}

@@ -28,20 +28,23 @@ __global__ __launch_bounds__(256) void k_permute(Fr* __restrict__ st, size_t n, 
     st[3 * i + 2] = f29_to_fr(s2);
 }
 
-template <uint32_t D>
+// COOP: one row per DPP quad (poseidon2_f29.hpp), for batches narrower than
+// the chip; otherwise one row per lane.
+template <uint32_t D, bool COOP>
 __global__ __launch_bounds__(256) void k_hash_rows1(const Fr* __restrict__ m, uint32_t w, size_t nrows,
                                                     Fr* __restrict__ out, const F29* __restrict__ rc, uint32_t rf,
                                                     uint32_t rp) {
-    const size_t i = gtid();
+    const size_t i = COOP ? (gtid() >> 2) : gtid();
     if (i >= nrows) return;
     const Fr* row = m + i * w;
-    out[i] = sponge_f29<D>([&](uint32_t k) { return row[k]; }, w, rc, rf, rp);
+    const Fr d = sponge_f29<D, COOP>([&](uint32_t k) { return row[k]; }, w, rc, rf, rp);
+    if (!COOP || (threadIdx.x & 3) == 0) out[i] = d;
 }
 
-template <uint32_t D>
+template <uint32_t D, bool COOP>
 __global__ __launch_bounds__(256) void k_hash_rows_multi(MatList ml, size_t nrows, Fr* __restrict__ out,
                                                          const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
-    const size_t i = gtid();
+    const size_t i = COOP ? (gtid() >> 2) : gtid();
     if (i >= nrows) return;
     uint32_t total = 0;
     for (uint32_t j = 0; j < ml.n; ++j) total += ml.width[j];
@@ -53,34 +56,39 @@ __global__ __launch_bounds__(256) void k_hash_rows_multi(MatList ml, size_t nrow
         }
         return ml.ptr[j][i * ml.width[j] + k];
     };
-    out[i] = sponge_f29<D>(get, total, rc, rf, rp);
+    const Fr d = sponge_f29<D, COOP>(get, total, rc, rf, rp);
+    if (!COOP || (threadIdx.x & 3) == 0) out[i] = d;
 }
 
-template <uint32_t D>
+template <uint32_t D, bool COOP>
 __global__ __launch_bounds__(256) void k_merkle_level(const Fr* __restrict__ src, Fr* __restrict__ dst, size_t nout,
                                                       const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
-    const size_t i = gtid();
+    const size_t i = COOP ? (gtid() >> 2) : gtid();
     if (i >= nout) return;
-    dst[i] = compress_f29<D>(src[2 * i], src[2 * i + 1], rc, rf, rp);
+    const Fr d = compress_f29<D, COOP>(src[2 * i], src[2 * i + 1], rc, rf, rp);
+    if (!COOP || (threadIdx.x & 3) == 0) dst[i] = d;
 }
 
-// Top of a tree in one workgroup: `len` (<= 2*blockDim, power of two) digests at
-// layers[off..off+len) -> every layer above them, through the LDS.
+// Top of a tree in one workgroup of 4 * 64 lanes: `len` (<= 128, power of
+// two) digests at layers[off..off+len) -> every layer above them, one
+// compression per DPP quad, through the LDS.
 template <uint32_t D>
-__global__ __launch_bounds__(64) void k_merkle_top(Fr* __restrict__ layers, size_t off, uint32_t len,
+__global__ __launch_bounds__(256) void k_merkle_top(Fr* __restrict__ layers, size_t off, uint32_t len,
                                                     const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
     __shared__ Fr buf[128];
     for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) buf[e] = layers[off + e];
     __syncthreads();
     size_t out_off = off + len;
+    const uint32_t q = threadIdx.x >> 2;
+    const bool lead = (threadIdx.x & 3) == 0;
     while (len > 1) {
         const uint32_t nout = len / 2;
         Fr r;
-        if (threadIdx.x < nout) r = compress_f29<D>(buf[2 * threadIdx.x], buf[2 * threadIdx.x + 1], rc, rf, rp);
+        if (q < nout) r = compress_f29<D, true>(buf[2 * q], buf[2 * q + 1], rc, rf, rp);
         __syncthreads();
-        if (threadIdx.x < nout) {
-            buf[threadIdx.x] = r;
-            layers[out_off + threadIdx.x] = r;
+        if (q < nout && lead) {
+            buf[q] = r;
+            layers[out_off + q] = r;
         }
         __syncthreads();
         out_off += nout;
@@ -129,6 +137,38 @@ hipError_t launch_rc_to_f29(const Fr* rc, F29* rc29, uint32_t n, hipStream_t st)
             hipLaunchKernelGGL(KERNEL<11>, __VA_ARGS__);                \
     } while (0)
 
+// (degree, coop) dispatch.  A batch of at most COOP_MAX permutations runs one
+// state per DPP quad: 4 * COOP_MAX lanes = one wave per SIMD of the 256 CUs,
+// where the quad form's shorter critical path (30 vs 46 S-boxes) wins; wider
+// batches are throughput-bound and keep one state per lane.
+#define LSP_DISPATCH_DC(L, COOP, KERNEL, ...)                             \
+    do {                                                                  \
+        if ((L).sbox_degree == 17) {                                      \
+            if (COOP)                                                     \
+                hipLaunchKernelGGL((KERNEL<17, true>), __VA_ARGS__);      \
+            else                                                          \
+                hipLaunchKernelGGL((KERNEL<17, false>), __VA_ARGS__);     \
+        } else {                                                          \
+            if (COOP)                                                     \
+                hipLaunchKernelGGL((KERNEL<11, true>), __VA_ARGS__);      \
+            else                                                          \
+                hipLaunchKernelGGL((KERNEL<11, false>), __VA_ARGS__);     \
+        }                                                                 \
+    } while (0)
+
+static constexpr size_t COOP_MAX = 16384;
+
+// grid for n states: quads in 64-lane blocks when coop, else 256-lane blocks
+static inline void state_grid(size_t n, bool coop, unsigned& blocks, unsigned& bs) {
+    if (coop) {
+        bs = 64;
+        blocks = nblocks(4 * n, bs);
+    } else {
+        bs = 256;
+        blocks = nblocks(n, bs);
+    }
+}
+
 hipError_t launch_permute(Fr* states, size_t n, const F29* rc, P2Layout L, hipStream_t st) {
     if (!n) return hipSuccess;
     LSP_DISPATCH_D(L, k_permute, dim3(nblocks(n, 256)), dim3(256), 0, st, states, n, rc, L.rounds_f, L.rounds_p);
@@ -137,13 +177,15 @@ hipError_t launch_permute(Fr* states, size_t n, const F29* rc, P2Layout L, hipSt
 
 hipError_t launch_hash_rows(const MatList& m, size_t nrows, Fr* out, const F29* rc, P2Layout L, hipStream_t st) {
     if (!nrows) return hipSuccess;
-    const unsigned bs = nrows >= (1u << 14) ? 256u : 64u;  // spread narrow batches over more CUs
+    const bool coop = nrows <= COOP_MAX;
+    unsigned blocks, bs;
+    state_grid(nrows, coop, blocks, bs);
     if (m.n == 1)
-        LSP_DISPATCH_D(L, k_hash_rows1, dim3(nblocks(nrows, bs)), dim3(bs), 0, st, m.ptr[0], m.width[0], nrows,
-                       out, rc, L.rounds_f, L.rounds_p);
+        LSP_DISPATCH_DC(L, coop, k_hash_rows1, dim3(blocks), dim3(bs), 0, st, m.ptr[0], m.width[0], nrows, out, rc,
+                        L.rounds_f, L.rounds_p);
     else
-        LSP_DISPATCH_D(L, k_hash_rows_multi, dim3(nblocks(nrows, bs)), dim3(bs), 0, st, m, nrows, out, rc,
-                       L.rounds_f, L.rounds_p);
+        LSP_DISPATCH_DC(L, coop, k_hash_rows_multi, dim3(blocks), dim3(bs), 0, st, m, nrows, out, rc, L.rounds_f,
+                        L.rounds_p);
     return hipGetLastError();
 }
 
@@ -157,29 +199,28 @@ hipError_t launch_grind(const Fr pre[3], uint32_t wlane, uint64_t base, uint64_t
 
 hipError_t launch_merkle_level(const Fr* src, Fr* dst, size_t nout, const F29* rc, P2Layout L, hipStream_t st) {
     if (!nout) return hipSuccess;
-    LSP_DISPATCH_D(L, k_merkle_level, dim3(nblocks(nout, 256)), dim3(256), 0, st, src, dst, nout, rc, L.rounds_f,
-                   L.rounds_p);
+    const bool coop = nout <= COOP_MAX;
+    unsigned blocks, bs;
+    state_grid(nout, coop, blocks, bs);
+    LSP_DISPATCH_DC(L, coop, k_merkle_level, dim3(blocks), dim3(bs), 0, st, src, dst, nout, rc, L.rounds_f,
+                    L.rounds_p);
     return hipGetLastError();
 }
 
 hipError_t launch_merkle_tree(Fr* layers, size_t nleaves, const F29* rc, P2Layout L, hipStream_t st) {
-    // Wide levels: one compression per lane, 256-lane blocks.  Narrow levels
-    // (< 2^14 nodes) are latency-bound (one permutation per level on the
-    // critical path): 64-lane blocks spread their waves over as many CUs as
-    // possible.  The last 64 -> 1 levels run in one wave.
+    // One launch per level down to 128 digests (launch_merkle_level picks the
+    // per-lane or per-quad form by width), then the last 128 -> 1 levels in
+    // one workgroup.
     size_t off = 0, len = nleaves;
-    while (len > 64) {
+    while (len > 128) {
         const size_t nout = len / 2;
-        const unsigned bs = nout >= (1u << 14) ? 256u : 64u;
-        LSP_DISPATCH_D(L, k_merkle_level, dim3(nblocks(nout, bs)), dim3(bs), 0, st, layers + off, layers + off + len,
-                       nout, rc, L.rounds_f, L.rounds_p);
-        hipError_t e = hipGetLastError();
+        hipError_t e = launch_merkle_level(layers + off, layers + off + len, nout, rc, L, st);
         if (e != hipSuccess) return e;
         off += len;
         len /= 2;
     }
     if (len > 1) {
-        LSP_DISPATCH_D(L, k_merkle_top, dim3(1), dim3(64), 0, st, layers, off, (uint32_t)len, rc, L.rounds_f,
+        LSP_DISPATCH_D(L, k_merkle_top, dim3(1), dim3(256), 0, st, layers, off, (uint32_t)len, rc, L.rounds_f,
                        L.rounds_p);
         return hipGetLastError();
     }

@@ -61,6 +61,68 @@ __device__ __forceinline__ void permute3_f29(F29& s0, F29& s1, F29& s2, const F2
     }
 }
 
+// ---- quad-cooperative permutation, for launches narrower than the chip.
+// One state lives in the 4 lanes of a DPP quad, replicated; in a full round
+// lane j (< 3; lane 3 mirrors lane 2) computes only S-box j and the quad
+// exchanges the three results with quad_perm broadcasts, so a full round costs
+// one S-box instead of three.  Partial rounds run redundantly in every lane.
+// Critical path: rf + rp S-boxes instead of 3 rf + rp (e.g. 30 vs 46); every
+// lane of the quad must be active.
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t x, int q) {
+    switch (q) {
+        case 0:
+            return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x00, 0xf, 0xf, false);
+        case 1:
+            return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x55, 0xf, 0xf, false);
+        default:
+            return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xaa, 0xf, 0xf, false);
+    }
+}
+
+__device__ __forceinline__ F29 f29_sel3(uint32_t j, const F29& a, const F29& b, const F29& c) {
+    // branch-free: masks instead of ?: (which the compiler turns into exec-mask branches)
+    const uint32_t m0 = 0u - (uint32_t)(j == 0), m1 = 0u - (uint32_t)(j == 1), m2 = ~(m0 | m1);
+    F29 r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.l[i] = (a.l[i] & m0) | (b.l[i] & m1) | (c.l[i] & m2);
+    return r;
+}
+
+template <uint32_t D>
+__device__ __forceinline__ void full_round_coop(F29& s0, F29& s1, F29& s2, const F29* __restrict__ c, uint32_t j) {
+    const F29 x = sbox29<D>(f29_sel3(j, f29_add(s0, c[0]), f29_add(s1, c[1]), f29_add(s2, c[2])));
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        s0.l[i] = quad_bcast(x.l[i], 0);
+        s1.l[i] = quad_bcast(x.l[i], 1);
+        s2.l[i] = quad_bcast(x.l[i], 2);
+    }
+    ext_layer29(s0, s1, s2);
+}
+
+template <uint32_t D>
+__device__ __forceinline__ void permute3_f29_coop(F29& s0, F29& s1, F29& s2, const F29* __restrict__ rc29,
+                                                  uint32_t rf, uint32_t rp) {
+    const uint32_t j = min(threadIdx.x & 3u, 2u);
+    const uint32_t half = rf / 2;
+    const F29* ini = rc29;
+    const F29* ter = rc29 + 3 * half;
+    const F29* itl = rc29 + 6 * half;
+    ext_layer29(s0, s1, s2);
+    for (uint32_t r = 0; r < half; ++r) full_round_coop<D>(s0, s1, s2, ini + 3 * r, j);
+    s1 = f29_reduce(s1);
+    s2 = f29_reduce(s2);
+    for (uint32_t r = 0; r < rp; ++r) {
+        s0 = sbox29<D>(f29_add(s0, itl[r]));
+        const F29 t = f29_reduce(f29_add(f29_add(s0, s1), s2));
+        s0 = f29_add(s0, t);
+        s1 = f29_add(s1, t);
+        s2 = f29_reduce(f29_add(f29_add(s2, s2), t));
+    }
+    s1 = f29_reduce(s1);
+    for (uint32_t r = 0; r < half; ++r) full_round_coop<D>(s0, s1, s2, ter + 3 * r, j);
+}
+
 __device__ __forceinline__ F29 f29_zero() {
     F29 z;
 #pragma unroll
@@ -68,29 +130,38 @@ __device__ __forceinline__ F29 f29_zero() {
     return z;
 }
 
+template <uint32_t D, bool COOP = false>
+__device__ __forceinline__ void permute3_any(F29& s0, F29& s1, F29& s2, const F29* __restrict__ rc29, uint32_t rf,
+                                             uint32_t rp) {
+    if (COOP)
+        permute3_f29_coop<D>(s0, s1, s2, rc29, rf, rp);
+    else
+        permute3_f29<D>(s0, s1, s2, rc29, rf, rp);
+}
+
 // PaddingFreeSponge<Perm,3,2,1>::hash_iter over n elements read as ark-form Fr
 // by get(k); returns the ark-form (canonical) digest
-template <uint32_t D, class Get>
+template <uint32_t D, bool COOP = false, class Get>
 __device__ __forceinline__ Fr sponge_f29(Get get, uint32_t n, const F29* rc29, uint32_t rf, uint32_t rp) {
     F29 s0 = f29_zero(), s1 = f29_zero(), s2 = f29_zero();
     uint32_t k = 0;
     while (k + 2 <= n) {
         s0 = f29_from_fr(get(k));
         s1 = f29_from_fr(get(k + 1));
-        permute3_f29<D>(s0, s1, s2, rc29, rf, rp);
+        permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp);
         k += 2;
     }
     if (k < n) {
         s0 = f29_from_fr(get(k));
-        permute3_f29<D>(s0, s1, s2, rc29, rf, rp);
+        permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp);
     }
     return f29_to_fr(s0);
 }
 
-template <uint32_t D>
+template <uint32_t D, bool COOP = false>
 __device__ __forceinline__ Fr compress_f29(const Fr& l, const Fr& r, const F29* rc29, uint32_t rf, uint32_t rp) {
     F29 s0 = f29_from_fr(l), s1 = f29_from_fr(r), s2 = f29_zero();
-    permute3_f29<D>(s0, s1, s2, rc29, rf, rp);
+    permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp);
     return f29_to_fr(s0);
 }
 

@@ -179,6 +179,23 @@ int lsp_batch_inverse(lsp_ctx *ctx, const lsp_fr *in, size_t n, lsp_fr *out, int
  * (bin/src/main.rs:78).  trace: h x w row-major. */
 int lsp_prove(lsp_ctx *ctx, const lsp_fr *trace, size_t h, size_t w, const int32_t *air, size_t air_len,
               const lsp_fr *public_values, size_t npub, int mem, lsp_proof **out);
+/* Sharded prove: one proof over G = 2^b ranks,
+ * G <= 2^log_blowup.  Rank g owns the LDE rows [g N/G, (g+1) N/G) -- whole
+ * cosets of the bit-reversed LDE, so a whole subtree of each input Merkle
+ * tree -- the quotient points whose rows it holds and a slice of every FRI
+ * vector; ranks exchange subtree roots, the quotient chunks, the opened
+ * values, short FRI vectors and the query openings.  The proof is
+ * byte-identical to lsp_prove's.
+ * In-process group: rank g = ctxs[g]; distinct devices (one host process
+ * driving the node's GPUs, exchanges device-to-device with peer access) or
+ * the same device repeated (virtual ranks).  traces[g] is rank g's copy of
+ * the trace (mem as in lsp_prove; device pointers on ctxs[g]'s device).
+ * Replaces p3_uni_stark::prove (bin/src/main.rs:80-86) like lsp_prove. */
+typedef struct lsp_group lsp_group;
+int lsp_group_create(lsp_ctx *const *ctxs, int n, lsp_group **out);
+int lsp_group_destroy(lsp_group *grp);
+int lsp_prove_group(lsp_group *grp, const lsp_fr *const *traces, size_t h, size_t w, const int32_t *air,
+                    size_t air_len, const lsp_fr *public_values, size_t npub, int mem, lsp_proof **out);
 /* serialized proof (format in DESIGN.md); buf == NULL -> *len = required size */
 int lsp_proof_serialize(const lsp_proof *proof, uint8_t *buf, size_t cap, size_t *len);
 int lsp_proof_free(lsp_proof *proof);

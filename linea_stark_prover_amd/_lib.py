@@ -82,6 +82,12 @@ _SIGS = {
     "lsp_proof_serialize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                            ctypes.POINTER(ctypes.c_size_t)]),
     "lsp_proof_free": (ctypes.c_int, [ctypes.c_void_p]),
+    "lsp_group_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_void_p)]),
+    "lsp_group_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "lsp_prove_group": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t,
+                                       ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, c_fr_p, ctypes.c_size_t,
+                                       ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "lsp_verify": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, c_fr_p, ctypes.c_size_t,
                                   ctypes.c_char_p, ctypes.c_size_t]),
     "lsp_last_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),

@@ -3,7 +3,9 @@
 
 #include <cstring>
 #include <memory>
+#include <thread>
 
+#include "comm.hpp"
 #include "prove_internal.hpp"
 
 using namespace lsp;
@@ -533,6 +535,100 @@ int lsp_prove(lsp_ctx* ctx, const lsp_fr* trace, size_t h, size_t w, const int32
         for (size_t i = 0; i < npub; ++i) pub[i] = to_fr(pubv[i]);
         const Fr* din = dev_in(ctx, trace, h * w, mem, "trace_in");
         *out = prove_device(ctx, din, h, w, A, pub.data(), npub);
+    });
+}
+
+// ------------------------------------------------------- sharded prove
+struct lsp_group {
+    std::vector<lsp_ctx*> ctxs;
+};
+
+int lsp_group_create(lsp_ctx* const* ctxs, int n, lsp_group** out) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(ctxs && out && n >= 1 && (n & (n - 1)) == 0, LSP_E_ARG, "a group is 2^b contexts");
+        auto* grp = new lsp_group();
+        grp->ctxs.assign(ctxs, ctxs + n);
+        for (lsp_ctx* c : grp->ctxs) {
+            if (!c || c->device == LSP_HOST_ONLY) {
+                delete grp;
+                throw LspError(LSP_E_ARG, "every group member needs a GPU context");
+            }
+        }
+        // peer access between the distinct devices (xGMI copies of the exchanges)
+        for (lsp_ctx* a : grp->ctxs)
+            for (lsp_ctx* b : grp->ctxs)
+                if (a->device != b->device) {
+                    LSP_HIP(hipSetDevice(a->device));
+                    int ok = 0;
+                    LSP_HIP(hipDeviceCanAccessPeer(&ok, a->device, b->device));
+                    if (ok) {
+                        hipError_t e = hipDeviceEnablePeerAccess(b->device, 0);
+                        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) LSP_HIP(e);
+                        (void)hipGetLastError();
+                    }
+                }
+        *out = grp;
+    });
+}
+
+int lsp_group_destroy(lsp_group* grp) {
+    delete grp;
+    return LSP_OK;
+}
+
+int lsp_prove_group(lsp_group* grp, const lsp_fr* const* traces, size_t h, size_t w, const int32_t* air,
+                    size_t air_len, const lsp_fr* pubv, size_t npub, int mem, lsp_proof** out) {
+    lsp_ctx* c0 = grp && !grp->ctxs.empty() ? grp->ctxs[0] : nullptr;
+    return guarded(c0, [&] {
+        LSP_REQUIRE(grp && traces && out && pubv, LSP_E_ARG, "bad prove_group arguments");
+        const int G = (int)grp->ctxs.size();
+        const Air A = Air::parse(air, air_len);
+        std::vector<Fr> pub(npub);
+        for (size_t i = 0; i < npub; ++i) pub[i] = to_fr(pubv[i]);
+        ThreadGroup tg(G);
+        for (int r = 0; r < G; ++r) tg.device[r] = grp->ctxs[r]->device;
+        std::vector<lsp_proof*> res(G, nullptr);
+        std::vector<int> code(G, LSP_OK);
+        std::vector<std::string> msg(G);
+        std::vector<std::thread> th;
+        for (int r = 0; r < G; ++r) {
+            th.emplace_back([&, r] {
+                lsp_ctx* ctx = grp->ctxs[r];
+                try {
+                    std::lock_guard<std::mutex> lk(ctx->mu);
+                    need_gpu(ctx);
+                    const Fr* din = dev_in(ctx, traces[r], h * w, mem, "trace_in");
+                    ThreadComm comm(&tg, r);
+                    res[r] = prove_shard(ctx, comm, din, h, w, A, pub.data(), npub);
+                } catch (const LspError& e) {
+                    code[r] = e.code;
+                    msg[r] = e.what();
+                    tg.abort();
+                } catch (const std::exception& e) {
+                    code[r] = LSP_E_STATE;
+                    msg[r] = e.what();
+                    tg.abort();
+                }
+            });
+        }
+        for (auto& t : th) t.join();
+        int bad = -1;
+        for (int r = 0; r < G && bad < 0; ++r)  // report the first rank that failed on its own
+            if (code[r] != LSP_OK && msg[r].find("another rank") == std::string::npos) bad = r;
+        for (int r = 0; r < G && bad < 0; ++r)
+            if (code[r] != LSP_OK) bad = r;
+        if (bad < 0) {
+            const std::vector<uint8_t> ref = serialize(*res[0]);
+            for (int r = 1; r < G; ++r)
+                if (serialize(*res[r]) != ref) {
+                    bad = r;
+                    code[r] = LSP_E_STATE;
+                    msg[r] = "ranks disagree on the proof";
+                }
+        }
+        for (int r = (bad < 0 ? 1 : 0); r < G; ++r) delete res[r];
+        if (bad >= 0) throw LspError(code[bad], "rank " + std::to_string(bad) + ": " + msg[bad]);
+        *out = res[0];
     });
 }
 

@@ -1,0 +1,123 @@
+// Exchange layer of the sharded prover.  A proof over G ranks
+// needs only two collectives, both on device buffers and both small except
+// the quotient-chunk exchange: allgather (subtree roots, quotient chunks,
+// the FRI vector once it is short, query openings) and broadcast (opened
+// values from rank 0).  The transcript runs redundantly on every rank, so
+// no challenge is ever sent.
+//
+//   SoloComm     G = 1 (the single-GPU prover; allgather is a copy)
+//   ThreadComm   G ranks of one process, one thread and one lsp_ctx each:
+//                distinct GPUs of the node (device-to-device copies over
+//                xGMI with peer access on) or the same GPU repeated
+//                ("virtual ranks", how the sharded path is tested on one GPU)
+//   RcclComm     one process per GPU over RCCL (comm_rccl.cpp)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "host.hpp"
+
+namespace lsp {
+
+struct Comm {
+    int rank = 0, size = 1;
+    virtual ~Comm() {}
+    // recv[r * bytes ...] = rank r's send (device buffers, ordered on ctx->stream)
+    virtual void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) = 0;
+    // every rank's buf = root's buf (device buffer)
+    virtual void bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) = 0;
+
+    // host-vector conveniences over the device collectives
+    std::vector<Fr> allgather_fr(lsp_ctx* ctx, const Fr* host, size_t n) {
+        Fr* s = ctx->fbuf("comm_send", n);
+        Fr* r = ctx->fbuf("comm_recv", n * (size_t)size);
+        LSP_HIP(hipMemcpyAsync(s, host, n * sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+        allgather(ctx, s, r, n * sizeof(Fr));
+        std::vector<Fr> out(n * (size_t)size);
+        LSP_HIP(hipMemcpyAsync(out.data(), r, out.size() * sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+        LSP_HIP(hipStreamSynchronize(ctx->stream));
+        return out;
+    }
+};
+
+struct SoloComm : Comm {
+    void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
+        if (send != recv)
+            LSP_HIP(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    void bcast(lsp_ctx*, void*, size_t, int) override {}
+};
+
+// Shared state of an in-process group: a generation barrier that any rank can
+// abort (a rank that throws must not leave the others waiting forever).
+struct ThreadGroup {
+    int size;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    bool aborted = false;
+    std::vector<const void*> slot;
+    std::vector<int> device;
+    explicit ThreadGroup(int n) : size(n), slot(n, nullptr), device(n, 0) {}
+    void barrier() {
+        std::unique_lock<std::mutex> lk(m);
+        if (aborted) throw LspError(LSP_E_STATE, "another rank of the group failed");
+        const uint64_t g = gen;
+        if (++arrived == size) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return;
+        }
+        cv.wait(lk, [&] { return gen != g || aborted; });
+        if (aborted) throw LspError(LSP_E_STATE, "another rank of the group failed");
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(m);
+        aborted = true;
+        cv.notify_all();
+    }
+};
+
+struct ThreadComm : Comm {
+    ThreadGroup* grp;
+    ThreadComm(ThreadGroup* g, int r) : grp(g) {
+        rank = r;
+        size = g->size;
+    }
+    void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
+        LSP_HIP(hipStreamSynchronize(ctx->stream));  // send is complete
+        grp->slot[rank] = send;
+        grp->barrier();
+        for (int r = 0; r < size; ++r) {
+            void* dst = (char*)recv + (size_t)r * bytes;
+            if (grp->device[r] == ctx->device)
+                LSP_HIP(hipMemcpyAsync(dst, grp->slot[r], bytes, hipMemcpyDeviceToDevice, ctx->stream));
+            else
+                LSP_HIP(hipMemcpyPeerAsync(dst, ctx->device, grp->slot[r], grp->device[r], bytes, ctx->stream));
+        }
+        LSP_HIP(hipStreamSynchronize(ctx->stream));
+        grp->barrier();  // peers may reuse their send buffers only after every copy
+    }
+    void bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) override {
+        LSP_HIP(hipStreamSynchronize(ctx->stream));
+        if (rank == root) grp->slot[root] = buf;
+        grp->barrier();
+        if (rank != root) {
+            if (grp->device[root] == ctx->device)
+                LSP_HIP(hipMemcpyAsync(buf, grp->slot[root], bytes, hipMemcpyDeviceToDevice, ctx->stream));
+            else
+                LSP_HIP(hipMemcpyPeerAsync(buf, ctx->device, grp->slot[root], grp->device[root], bytes, ctx->stream));
+            LSP_HIP(hipStreamSynchronize(ctx->stream));
+        }
+        grp->barrier();
+    }
+};
+
+}  // namespace lsp

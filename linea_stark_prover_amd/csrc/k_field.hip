@@ -51,6 +51,16 @@ __global__ __launch_bounds__(256) void k_gather(const uint64_t* __restrict__ ptr
     const size_t i = gtid();
     if (i < n) out[i] = *reinterpret_cast<const Fr*>(ptrs[i]);
 }
+
+__global__ __launch_bounds__(256) void k_assemble_chunks(const Fr* __restrict__ stage, uint32_t logGq, size_t cpr,
+                                                         size_t h, Fr* __restrict__ out) {
+    const size_t t = gtid();
+    const size_t q = cpr << logGq;
+    if (t >= h * q) return;
+    const size_t k = t / q, j = t - k * q;
+    const size_t r = brev_bits(j & ((1ull << logGq) - 1), logGq), c = j >> logGq;
+    out[t] = stage[(r * h + k) * cpr + c];
+}
 }  // namespace
 
 hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st) {
@@ -68,6 +78,12 @@ hipError_t launch_calib_mul(Fr* out, size_t nthreads, uint32_t iters, hipStream_
 hipError_t launch_gather(const uint64_t* ptrs, Fr* out, size_t n, hipStream_t st) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_gather, dim3(nblocks(n, 256)), dim3(256), 0, st, ptrs, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_assemble_chunks(const Fr* stage, uint32_t logGq, size_t cpr, size_t h, Fr* out, hipStream_t st) {
+    const size_t n = h * (cpr << logGq);
+    hipLaunchKernelGGL(k_assemble_chunks, dim3(nblocks(n, 256)), dim3(256), 0, st, stage, logGq, cpr, h, out);
     return hipGetLastError();
 }
 

@@ -170,7 +170,7 @@ void plan_passes(uint32_t logH, uint32_t kmax, uint32_t* ks, uint32_t& np) {
 }
 }  // namespace
 
-hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t added_bits, const Fr* tw_inv,
+hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t ncosets, const Fr* tw_inv,
                       const Fr* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
                       hipStream_t st) {
     if (w == 0) return hipSuccess;
@@ -228,7 +228,7 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
         // h = 1: the coefficient is the value; every coset row equals it
         hipError_t e = hipMemcpyAsync(X, in, w * sizeof(Fr), hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) return e;
-        for (uint32_t k = 0; k < (1u << added_bits); ++k) {
+        for (uint32_t k = 0; k < ncosets; ++k) {
             e = hipMemcpyAsync(out + (size_t)k * w, X, w * sizeof(Fr), hipMemcpyDeviceToDevice, st);
             if (e != hipSuccess) return e;
         }
@@ -236,7 +236,7 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
     }
     hipError_t e = run(false, 1, in, X, tw_inv, PASS_INV_FIRST);
     if (e != hipSuccess) return e;
-    return run(true, 1u << added_bits, X, out, tw_fwd, PASS_FWD_FIRST);
+    return run(true, ncosets, X, out, tw_fwd, PASS_FWD_FIRST);
 }
 
 hipError_t launch_pow_tables(const Fr* bases, size_t nbases, uint32_t L1, uint32_t L2, const Fr* scale, Fr* tabs,

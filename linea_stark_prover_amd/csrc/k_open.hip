@@ -9,10 +9,11 @@ namespace lsp {
 
 namespace {
 __global__ __launch_bounds__(256) void k_open_denoms(Fr z, Fr gen, const Fr* __restrict__ tabN, uint32_t L1,
-                                                     uint32_t logN, size_t n, Fr* __restrict__ den) {
+                                                     uint32_t logN, size_t n, uint64_t row0,
+                                                     Fr* __restrict__ den) {
     const size_t i = gtid();
     if (i >= n) return;
-    den[i] = fr_sub(z, fr_mul(gen, pow2l(tabN, L1, brev_bits(i, logN))));
+    den[i] = fr_sub(z, fr_mul(gen, pow2l(tabN, L1, brev_bits(row0 + i, logN))));
 }
 
 constexpr uint32_t INTERP_ROWS = 1024;  // rows per block
@@ -74,17 +75,18 @@ __global__ __launch_bounds__(256) void k_reduce_rows(ReduceArgs a) {
 
 __global__ __launch_bounds__(256) void k_fri_fold(const Fr* __restrict__ v, size_t m, Fr half, Fr half_beta,
                                                   const Fr* __restrict__ tab, uint32_t L1, uint32_t logm,
-                                                  Fr* __restrict__ out) {
+                                                  uint64_t i0, Fr* __restrict__ out) {
     const size_t i = gtid();
     if (i >= m) return;
-    const Fr p = fr_mul(half_beta, pow2l(tab, L1, brev_bits(i, logm)));
+    const Fr p = fr_mul(half_beta, pow2l(tab, L1, brev_bits(i0 + i, logm)));
     out[i] = fr_add(fr_mul(fr_add(half, p), v[2 * i]), fr_mul(fr_sub(half, p), v[2 * i + 1]));
 }
 }  // namespace
 
 hipError_t launch_open_denoms(Fr z, Fr gen, const Fr* tabN, uint32_t L1, uint32_t logN, size_t n, Fr* den,
-                              hipStream_t st) {
-    hipLaunchKernelGGL(k_open_denoms, dim3(nblocks(n, 256)), dim3(256), 0, st, z, gen, tabN, L1, logN, n, den);
+                              hipStream_t st, uint64_t row0) {
+    hipLaunchKernelGGL(k_open_denoms, dim3(nblocks(n, 256)), dim3(256), 0, st, z, gen, tabN, L1, logN, n, row0,
+                       den);
     return hipGetLastError();
 }
 
@@ -107,10 +109,13 @@ hipError_t launch_reduce_rows(const ReduceArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_fri_fold(const Fr* v, size_t m, Fr half, Fr half_beta, const Fr* tab, uint32_t L1, Fr* out,
-                           hipStream_t st) {
-    uint32_t logm = 0;
-    while ((1ull << logm) < m) ++logm;
-    hipLaunchKernelGGL(k_fri_fold, dim3(nblocks(m, 256)), dim3(256), 0, st, v, m, half, half_beta, tab, L1, logm,
+                           hipStream_t st, uint64_t i0, int logm) {
+    uint32_t lg = 0;
+    if (logm >= 0)
+        lg = (uint32_t)logm;
+    else
+        while ((1ull << lg) < m) ++lg;
+    hipLaunchKernelGGL(k_fri_fold, dim3(nblocks(m, 256)), dim3(256), 0, st, v, m, half, half_beta, tab, L1, lg, i0,
                        out);
     return hipGetLastError();
 }

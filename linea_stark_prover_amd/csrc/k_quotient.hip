@@ -22,28 +22,31 @@ __device__ __forceinline__ Fr horner(const Fr* __restrict__ row, const int32_t* 
 }
 
 __global__ __launch_bounds__(256) void k_selector_denoms(const Fr* __restrict__ tabQ, uint32_t L1, Fr gen,
-                                                         Fr wh_inv, size_t Q, Fr* __restrict__ den) {
-    const size_t i = gtid();
-    if (i >= Q) return;
+                                                         Fr wh_inv, size_t n, uint64_t i0, uint32_t log_step,
+                                                         Fr* __restrict__ den) {
+    const size_t m = gtid();
+    if (m >= n) return;
+    const uint64_t i = i0 + ((uint64_t)m << log_step);
     const Fr x = fr_mul(gen, pow2l(tabQ, L1, i));
-    den[i] = fr_mul(fr_sub(x, fr_one()), fr_sub(x, wh_inv));
+    den[m] = fr_mul(fr_sub(x, fr_one()), fr_sub(x, wh_inv));
 }
 
 __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
-    const size_t i = gtid();
+    const size_t m = gtid();
     const size_t Q = 1ull << a.logQ;
-    if (i >= Q) return;
+    if (m >= (a.n ? a.n : Q)) return;
+    const uint64_t i = a.i0 + ((uint64_t)m << a.log_step);
     const uint32_t qmask = (1u << a.log_q) - 1;
     const Fr one = fr_one();
     const Fr x = fr_mul(a.gen, pow2l(a.tabQ, a.L1, i));
     const Fr xm1 = fr_sub(x, one);
     const Fr xml = fr_sub(x, a.wh_inv);
     const Fr zh = a.zh[i & qmask];
-    const Fr first = fr_mul(zh, fr_mul(xml, a.inv_den[i]));  // Z_H / (x - 1)
-    const Fr last = fr_mul(zh, fr_mul(xm1, a.inv_den[i]));   // Z_H / (x - w^-1)
+    const Fr first = fr_mul(zh, fr_mul(xml, a.inv_den[m]));  // Z_H / (x - 1)
+    const Fr last = fr_mul(zh, fr_mul(xm1, a.inv_den[m]));   // Z_H / (x - w^-1)
     const Fr trans = xml;                                    // x - w^-1
-    const Fr* loc = a.lde + brev_bits(i, a.logQ) * a.w;
-    const Fr* nxt = a.lde + brev_bits((i + (1ull << a.log_q)) & (Q - 1), a.logQ) * a.w;
+    const Fr* loc = a.lde + (brev_bits(i, a.logQ) - a.row0) * a.w;
+    const Fr* nxt = a.lde + (brev_bits((i + (1ull << a.log_q)) & (Q - 1), a.logQ) - a.row0) * a.w;
     const Fr ap = a.pub_alpha, dl = a.pub_delta, al = a.alpha;
     Fr acc = fr_zero();
 #define PUSH(X) acc = fr_add(fr_mul(acc, al), (X))
@@ -98,19 +101,20 @@ __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
         }
     }
 #undef PUSH
-    a.out[i] = fr_mul(acc, a.inv_zh[i & qmask]);
+    a.out[m] = fr_mul(acc, a.inv_zh[i & qmask]);
 }
 }  // namespace
 
-hipError_t launch_selector_denoms(const Fr* tabQ, uint32_t L1, Fr gen, Fr wh_inv, size_t Q, Fr* den,
-                                  hipStream_t st) {
-    hipLaunchKernelGGL(k_selector_denoms, dim3(nblocks(Q, 256)), dim3(256), 0, st, tabQ, L1, gen, wh_inv, Q, den);
+hipError_t launch_selector_denoms(const Fr* tabQ, uint32_t L1, Fr gen, Fr wh_inv, size_t n, Fr* den,
+                                  hipStream_t st, uint64_t i0, uint32_t log_step) {
+    hipLaunchKernelGGL(k_selector_denoms, dim3(nblocks(n, 256)), dim3(256), 0, st, tabQ, L1, gen, wh_inv, n, i0,
+                       log_step, den);
     return hipGetLastError();
 }
 
 hipError_t launch_quotient(const QuotientArgs& a, hipStream_t st) {
-    const size_t Q = 1ull << a.logQ;
-    hipLaunchKernelGGL(k_quotient, dim3(nblocks(Q, 256)), dim3(256), 0, st, a);
+    const size_t n = a.n ? a.n : (1ull << a.logQ);
+    hipLaunchKernelGGL(k_quotient, dim3(nblocks(n, 256)), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

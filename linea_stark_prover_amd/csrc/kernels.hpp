@@ -12,12 +12,12 @@
 namespace lsp {
 
 // ------------------------------------------------------------ k_ntt.hip
-// Bit-reversed coset LDE of the h x w row-major matrix `in` into the
-// (h << added_bits) x w row-major `out` (block k = coset k), via X (h x w
-// scratch, left holding h * coefficients).  tw_inv / tw_fwd: w_h^-x / w_h^x,
+// Coset evaluations of the h x w row-major matrix `in`: `ncosets` blocks of h
+// rows (block k on the coset of twist table k), each in bit-reversed order,
+// into row-major `out`, via X (h x w scratch, left holding h * coefficients).  tw_inv / tw_fwd: w_h^-x / w_h^x,
 // x < h/2.  twist: two-level tables (L1, L2) of base s and scale 1/h, one per
 // coset (twist_per_col = 0) or per (coset, column) at index k*w + c.
-hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t added_bits, const Fr* tw_inv,
+hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t ncosets, const Fr* tw_inv,
                       const Fr* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
                       hipStream_t st);
 // Two-level power tables: for each base b,
@@ -53,6 +53,10 @@ hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st)
 hipError_t launch_calib_mul(Fr* out, size_t nthreads, uint32_t iters, hipStream_t st);
 // out[i] = *ptrs[i]
 hipError_t launch_gather(const uint64_t* ptrs, Fr* out, size_t n, hipStream_t st);
+// Sharded quotient exchange: stage holds 2^logGq blocks of h x cpr values,
+// block r = chunks j = bitrev(r) + (c << logGq), c < cpr; out = the natural
+// h x q chunk matrix (q = cpr << logGq), out[k*q + j].
+hipError_t launch_assemble_chunks(const Fr* stage, uint32_t logGq, size_t cpr, size_t h, Fr* out, hipStream_t st);
 
 // ----------------------------------------------------- k_quotient.hip
 struct QuotientArgs {
@@ -68,18 +72,25 @@ struct QuotientArgs {
     uint32_t L1;
     const Fr* zh;       // q values of Z_H on the coset (index i mod q)
     const Fr* inv_zh;   // their inverses
-    const Fr* inv_den;  // 1/((x-1)(x-w_h^-1)) per point
-    Fr* out;            // Q values
+    const Fr* inv_den;  // 1/((x-1)(x-w_h^-1)) per computed point
+    Fr* out;            // one value per computed point
+    // Sharded evaluation: the points computed are i = i0 + (m << log_step),
+    // m < n (n = 0: all Q points), and `lde` holds the LDE rows from global
+    // row `row0` on.  Defaults: every point, the whole LDE.
+    uint64_t i0 = 0;
+    uint32_t log_step = 0;
+    uint64_t row0 = 0;
+    uint64_t n = 0;
 };
-// den[i] = (x_i - 1)(x_i - w_h^-1), x_i = GEN * w_Q^i
-hipError_t launch_selector_denoms(const Fr* tabQ, uint32_t L1, Fr gen, Fr wh_inv, size_t Q, Fr* den,
-                                  hipStream_t st);
+// den[m] = (x_i - 1)(x_i - w_h^-1), x_i = GEN * w_Q^i, i = i0 + (m << log_step), m < n
+hipError_t launch_selector_denoms(const Fr* tabQ, uint32_t L1, Fr gen, Fr wh_inv, size_t n, Fr* den,
+                                  hipStream_t st, uint64_t i0 = 0, uint32_t log_step = 0);
 hipError_t launch_quotient(const QuotientArgs& a, hipStream_t st);
 
 // --------------------------------------------------------- k_open.hip
-// den[i] = z - GEN * w_N^bitrev(i) for i < n (two-level table of w_N)
+// den[i] = z - GEN * w_N^bitrev(row0 + i) for i < n (two-level table of w_N)
 hipError_t launch_open_denoms(Fr z, Fr gen, const Fr* tabN, uint32_t L1, uint32_t logN, size_t n, Fr* den,
-                              hipStream_t st);
+                              hipStream_t st, uint64_t row0 = 0);
 // partial sums for barycentric interpolation over rows [0, h):
 // partial[b*w + c] = sum_{i in block b} M[i][c] * x_i * inv_den[i]
 hipError_t launch_interp_partial(const Fr* M, uint32_t w, size_t h, const Fr* inv_den, Fr gen, const Fr* tabN,
@@ -100,8 +111,10 @@ struct ReduceArgs {
     size_t n;
 };
 hipError_t launch_reduce_rows(const ReduceArgs& a, hipStream_t st);
-// FRI fold of v (2m values) -> out (m values); tab: two-level table of w_{2m}^-1
+// FRI fold of v (2m values) -> out (m values); tab: two-level table of w_{2M}^-1
+// where M = 2^logm is the whole folded length (logm < 0: M = m) and v holds
+// the pairs from global pair index i0 on (a shard of the vector).
 hipError_t launch_fri_fold(const Fr* v, size_t m, Fr half, Fr half_beta, const Fr* tab, uint32_t L1,
-                           Fr* out, hipStream_t st);
+                           Fr* out, hipStream_t st, uint64_t i0 = 0, int logm = -1);
 
 }  // namespace lsp

@@ -7,8 +7,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
+#include "comm.hpp"
 #include "host.hpp"
 #include "prove_internal.hpp"
 
@@ -79,10 +81,15 @@ Fr d2h_fr(lsp_ctx* ctx, const Fr* d) {
 }  // namespace
 
 // ----------------------------------------------------------------- LDE
+// Coset blocks [k0, k0 + nk) of the bit-reversed LDE (nk = 0: all
+// 2^added_bits): block k = rows k*h .. (k+1)*h - 1 of the full LDE, the
+// evaluations on shift_c * w_N^bitrev(k) * H_h.  d_out receives nk blocks.
 void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added_bits, const Fr* shifts_host,
-                Fr* d_out) {
+                Fr* d_out, uint32_t k0, uint32_t nk) {
     const uint32_t logh = log2_exact(h);
     const uint32_t B = 1u << added_bits;
+    if (nk == 0) nk = B;
+    LSP_REQUIRE(k0 + nk <= B, LSP_E_ARG, "coset range outside the LDE");
     const uint32_t logN = logh + added_bits;
     LSP_REQUIRE(logN <= 47, LSP_E_SIZE, "LDE larger than the 2-adic subgroup");
     Fr* X = ctx->fbuf("lde_X", h * w);
@@ -93,9 +100,9 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
     const size_t per_coset = shared ? 1 : w;
     const Fr wN = host_two_adic_generator(logN);
     const Fr hinv = fr_inv(fr_from_u64(h));
-    std::vector<Fr> bases((size_t)B * per_coset), scales((size_t)B * per_coset, hinv);
-    for (uint32_t k = 0; k < B; ++k) {
-        const Fr ck = fr_pow_u64(wN, host_bitrev(k, added_bits));
+    std::vector<Fr> bases((size_t)nk * per_coset), scales((size_t)nk * per_coset, hinv);
+    for (uint32_t k = 0; k < nk; ++k) {
+        const Fr ck = fr_pow_u64(wN, host_bitrev(k0 + k, added_bits));
         for (size_t c = 0; c < per_coset; ++c) bases[k * per_coset + c] = fr_mul(shifts_host[c], ck);
     }
     uint32_t L1, L2;
@@ -107,8 +114,8 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
     const size_t per = (1ull << L1) + (1ull << L2);
     Fr* tabs = ctx->fbuf("lde_tabs", per * bases.size());
     LSP_HIP(launch_pow_tables(dbases, bases.size(), L1, L2, dbases + bases.size(), tabs, st));
-    LSP_HIP(launch_lde(d_in, X, d_out, w, logh, added_bits, ctx->twiddle(logh, true), ctx->twiddle(logh, false), tabs,
-                       L1, L2, shared ? 0 : 1, st));
+    LSP_HIP(launch_lde(d_in, X, d_out, w, logh, nk, ctx->twiddle(logh, true), ctx->twiddle(logh, false), tabs, L1,
+                       L2, shared ? 0 : 1, st));
     // host vectors (bases, scales) must outlive the async copies
     LSP_HIP(hipStreamSynchronize(st));
 }
@@ -126,11 +133,6 @@ static MatList one_mat(const Fr* p, uint32_t w) {
     m.width[0] = w;
     m.n = 1;
     return m;
-}
-
-static void tree_path(const std::vector<Fr>& got, size_t& cur, uint32_t lg, std::vector<Fr>& out) {
-    out.assign(got.begin() + cur, got.begin() + cur + lg);
-    cur += lg;
 }
 
 // --------------------------------------------------------------- grind
@@ -183,8 +185,35 @@ uint64_t grind_device(lsp_ctx* ctx, Challenger& ch, uint32_t bits) {
 }
 
 // ------------------------------------------------------------- prove
-lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, const Air& air, const Fr* pub,
-                        size_t npub) {
+// Root of a Merkle tree whose 2^b bottom subtrees live on the 2^b ranks
+// (rank r's subtree root = `local`, leaves r*S .. (r+1)*S - 1).  `top` gets
+// the b + 1 host layers above the subtrees (top[0] = the rank roots).
+static Fr shard_root(lsp_ctx* ctx, Comm& comm, const Fr& local, std::vector<std::vector<Fr>>& top) {
+    if (comm.size == 1) {
+        top.assign(1, std::vector<Fr>(1, local));
+        return local;
+    }
+    top.assign(1, comm.allgather_fr(ctx, &local, 1));
+    while (top.back().size() > 1) {
+        const std::vector<Fr>& lo = top.back();
+        std::vector<Fr> up(lo.size() / 2);
+        for (size_t i = 0; i < up.size(); ++i) up[i] = ctx->p2.compress(lo[2 * i], lo[2 * i + 1]);
+        top.push_back(std::move(up));
+    }
+    return top.back()[0];
+}
+
+// p3_uni_stark::prove (bin/src/main.rs:80-86) as one rank of a G-rank
+// proof; G = 1 is the single-GPU prover.  Rank g owns the
+// LDE rows [g S, (g+1) S), S = N / G: whole cosets of the bit-reversed LDE
+// (G <= blowup), hence a whole subtree of every input Merkle tree, the
+// quotient points whose rows it holds, and a contiguous slice of every FRI
+// vector.  Exchanges: subtree roots, the quotient chunks (one allgather),
+// the opened values (broadcast from rank 0, which holds the low coset), the
+// FRI vector once a slice is shorter than FRI_SHARD_MIN, and the query
+// openings.  The transcript runs on every rank with identical inputs.
+lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, size_t w, const Air& air,
+                       const Fr* pub, size_t npub) {
     LSP_REQUIRE(npub >= 2, LSP_E_ARG, "public values must hold [alpha, delta]");
     LSP_REQUIRE(air.max_col < w, LSP_E_ARG, "AIR column id outside the trace width");
     const uint32_t log_h = log2_exact(h);
@@ -196,6 +225,12 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
     const uint32_t logN = log_h + lb, logQ = log_h + log_q;
     const size_t N = (size_t)1 << logN, Q = (size_t)1 << logQ;
     LSP_REQUIRE(logN <= 40, LSP_E_SIZE, "trace too large");
+    const uint32_t G = (uint32_t)comm.size, g = (uint32_t)comm.rank;
+    const uint32_t b = log2_exact(G);
+    LSP_REQUIRE(b <= lb, LSP_E_ARG, "a proof shards over at most 2^log_blowup ranks");
+    const uint32_t logS = logN - b;
+    const size_t S = N >> b, row0 = (size_t)g * S;
+    const uint32_t nk = 1u << (lb - b), k0 = g * nk;  // this rank's cosets
     hipStream_t st = ctx->stream;
     const Fr GEN = host_generator();
     const Fr one = fr_one();
@@ -208,14 +243,15 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
         T.begin("prove");
         // ---- commit to trace data
         T.begin("commit to trace data");
-        Fr* lde = ctx->fbuf("t_lde", N * w);
+        Fr* lde = ctx->fbuf("t_lde", S * w);
         std::vector<Fr> shifts(std::max(w, q), GEN);
         T.begin("coset_lde_batch");
-        lde_device(ctx, d_trace, h, w, lb, shifts.data(), lde);
+        lde_device(ctx, d_trace, h, w, lb, shifts.data(), lde, k0, nk);
         T.end("coset_lde_batch");
-        Fr* tlay = ctx->fbuf("t_tree", 2 * N - 1);
+        Fr* tlay = ctx->fbuf("t_tree", 2 * S - 1);
+        std::vector<std::vector<Fr>> ttop, qtop;
         T.begin("merkle tree");
-        proof->troot = commit_device(ctx, one_mat(lde, (uint32_t)w), N, tlay);
+        proof->troot = shard_root(ctx, comm, commit_device(ctx, one_mat(lde, (uint32_t)w), S, tlay), ttop);
         T.end("merkle tree");
         T.end("commit to trace data");
 
@@ -225,51 +261,71 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
         for (size_t i = 0; i < npub; ++i) ch.observe(pub[i]);
         const Fr alpha = ch.sample();
 
-        // ---- quotient
+        // ---- quotient.  Point i reads LDE rows bitrev_Q(i) and bitrev_Q(i + q):
+        // the ranks holding the first Q rows (Gq of them) each own the points
+        // i = bitrev(g) mod Gq, which are whole chunks j = i mod q (Gq <= q).
         T.begin("compute quotient polynomial");
+        const size_t Sq = std::min(S, Q), Gq = Q / Sq, cpr = q / Gq;
+        const uint32_t logGq = log2_exact(Gq);
         uint32_t L1Q;
         const Fr* tabQ = pow_table(ctx, "tabQ", host_two_adic_generator(logQ), logQ, L1Q);
         const Fr wh = host_two_adic_generator(log_h);
         const Fr wh_inv = fr_inv(wh);
-        Fr* den = ctx->fbuf("q_den", Q);
-        Fr* inv_den = ctx->fbuf("q_invden", Q);
-        LSP_HIP(launch_selector_denoms(tabQ, L1Q, GEN, wh_inv, Q, den, st));
-        LSP_HIP(launch_batch_inverse(den, inv_den, Q, st));
+        Fr* qv = ctx->fbuf("q_values", Q);  // the h x q chunk matrix, on every rank
+        Fr* qloc = G == 1 ? qv : ctx->fbuf("q_local", Sq);
         std::vector<Fr> zh(q), izh(q);
-        {
-            const Fr gh = fr_pow_u64(GEN, h), gq = host_two_adic_generator(log_q);
-            Fr g = one;
-            for (size_t k = 0; k < q; ++k) {
-                zh[k] = fr_sub(fr_mul(gh, g), one);
-                izh[k] = fr_inv(zh[k]);
-                g = fr_mul(g, gq);
+        if (row0 < Q) {
+            const uint64_t i0 = host_bitrev(g, logGq);
+            Fr* den = ctx->fbuf("q_den", Sq);
+            Fr* inv_den = ctx->fbuf("q_invden", Sq);
+            LSP_HIP(launch_selector_denoms(tabQ, L1Q, GEN, wh_inv, Sq, den, st, i0, logGq));
+            LSP_HIP(launch_batch_inverse(den, inv_den, Sq, st));
+            {
+                const Fr gh = fr_pow_u64(GEN, h), gq = host_two_adic_generator(log_q);
+                Fr x = one;
+                for (size_t k = 0; k < q; ++k) {
+                    zh[k] = fr_sub(fr_mul(gh, x), one);
+                    izh[k] = fr_inv(zh[k]);
+                    x = fr_mul(x, gq);
+                }
             }
+            Fr* dzh = ctx->fbuf("q_zh", 2 * q);
+            LSP_HIP(hipMemcpyAsync(dzh, zh.data(), q * sizeof(Fr), hipMemcpyHostToDevice, st));
+            LSP_HIP(hipMemcpyAsync(dzh + q, izh.data(), q * sizeof(Fr), hipMemcpyHostToDevice, st));
+            int32_t* dair = (int32_t*)ctx->buf("air", air.raw.size() * sizeof(int32_t));
+            LSP_HIP(
+                hipMemcpyAsync(dair, air.raw.data(), air.raw.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+            QuotientArgs qa;
+            qa.lde = lde;
+            qa.w = (uint32_t)w;
+            qa.logQ = logQ;
+            qa.log_q = log_q;
+            qa.air = dair;
+            qa.air_len = (uint32_t)air.raw.size();
+            qa.pub_alpha = pub[0];
+            qa.pub_delta = pub[1];
+            qa.alpha = alpha;
+            qa.gen = GEN;
+            qa.wh_inv = wh_inv;
+            qa.tabQ = tabQ;
+            qa.L1 = L1Q;
+            qa.zh = dzh;
+            qa.inv_zh = dzh + q;
+            qa.inv_den = inv_den;
+            qa.out = qloc;
+            qa.i0 = i0;
+            qa.log_step = logGq;
+            qa.row0 = row0;
+            qa.n = Sq;
+            LSP_HIP(launch_quotient(qa, st));
+            LSP_HIP(hipStreamSynchronize(st));  // zh/izh host vectors
         }
-        Fr* dzh = ctx->fbuf("q_zh", 2 * q);
-        LSP_HIP(hipMemcpyAsync(dzh, zh.data(), q * sizeof(Fr), hipMemcpyHostToDevice, st));
-        LSP_HIP(hipMemcpyAsync(dzh + q, izh.data(), q * sizeof(Fr), hipMemcpyHostToDevice, st));
-        int32_t* dair = (int32_t*)ctx->buf("air", air.raw.size() * sizeof(int32_t));
-        LSP_HIP(hipMemcpyAsync(dair, air.raw.data(), air.raw.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
-        Fr* qv = ctx->fbuf("q_values", Q);
-        QuotientArgs qa;
-        qa.lde = lde;
-        qa.w = (uint32_t)w;
-        qa.logQ = logQ;
-        qa.log_q = log_q;
-        qa.air = dair;
-        qa.air_len = (uint32_t)air.raw.size();
-        qa.pub_alpha = pub[0];
-        qa.pub_delta = pub[1];
-        qa.alpha = alpha;
-        qa.gen = GEN;
-        qa.wh_inv = wh_inv;
-        qa.tabQ = tabQ;
-        qa.L1 = L1Q;
-        qa.zh = dzh;
-        qa.inv_zh = dzh + q;
-        qa.inv_den = inv_den;
-        qa.out = qv;
-        LSP_HIP(launch_quotient(qa, st));
+        if (G > 1) {
+            // rank r < Gq holds chunks j = bitrev(r) + Gq c as an h x cpr matrix
+            Fr* stage = ctx->fbuf("q_stage", Sq * G);
+            comm.allgather(ctx, qloc, stage, Sq * sizeof(Fr));
+            LSP_HIP(launch_assemble_chunks(stage, logGq, cpr, h, qv, st));
+        }
         T.end("compute quotient polynomial");
 
         // ---- commit to quotient chunks: qv is the h x q matrix of chunks
@@ -282,12 +338,12 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
                 s = fr_mul(s, gQinv);
             }
         }
-        Fr* qlde = ctx->fbuf("q_lde", N * q);
+        Fr* qlde = ctx->fbuf("q_lde", S * q);
         T.begin("coset_lde_batch (quotient)");
-        lde_device(ctx, qv, h, q, lb, shifts.data(), qlde);
+        lde_device(ctx, qv, h, q, lb, shifts.data(), qlde, k0, nk);
         T.end("coset_lde_batch (quotient)");
-        Fr* qlay = ctx->fbuf("q_tree", 2 * N - 1);
-        proof->qroot = commit_device(ctx, one_mat(qlde, (uint32_t)q), N, qlay);
+        Fr* qlay = ctx->fbuf("q_tree", 2 * S - 1);
+        proof->qroot = shard_root(ctx, comm, commit_device(ctx, one_mat(qlde, (uint32_t)q), S, qlay), qtop);
         T.end("commit to quotient poly chunks");
         ch.observe(proof->qroot);
         const Fr zeta = ch.sample();
@@ -299,26 +355,29 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
         T.begin("compute_inverse_denominators");
         uint32_t L1N;
         const Fr* tabN = pow_table(ctx, "tabN", host_two_adic_generator(logN), logN, L1N);
-        Fr* dtmp = ctx->fbuf("o_den", N);
-        Fr* inv_z = ctx->fbuf("o_invz", N);
-        Fr* inv_zn = ctx->fbuf("o_invzn", N);
-        LSP_HIP(launch_open_denoms(zeta, GEN, tabN, L1N, logN, N, dtmp, st));
-        LSP_HIP(launch_batch_inverse(dtmp, inv_z, N, st));
-        LSP_HIP(launch_open_denoms(zeta_next, GEN, tabN, L1N, logN, N, dtmp, st));
-        LSP_HIP(launch_batch_inverse(dtmp, inv_zn, N, st));
+        Fr* dtmp = ctx->fbuf("o_den", S);
+        Fr* inv_z = ctx->fbuf("o_invz", S);
+        Fr* inv_zn = ctx->fbuf("o_invzn", S);
+        LSP_HIP(launch_open_denoms(zeta, GEN, tabN, L1N, logN, S, dtmp, st, row0));
+        LSP_HIP(launch_batch_inverse(dtmp, inv_z, S, st));
+        LSP_HIP(launch_open_denoms(zeta_next, GEN, tabN, L1N, logN, S, dtmp, st, row0));
+        LSP_HIP(launch_batch_inverse(dtmp, inv_zn, S, st));
         T.end("compute_inverse_denominators");
         T.begin("compute opened values with Lagrange interpolation");
-        // barycentric sums on the low coset (first h rows), then the host-side factor
+        // barycentric sums on the low coset (first h rows: rank 0), then the host-side factor
         const size_t maxw = std::max(w, q);
-        Fr* partial = ctx->fbuf("o_partial", ((h + 1023) / 1024) * maxw);
         Fr* sums = ctx->fbuf("o_sums", 2 * w + q);
-        uint32_t nb = 0;
-        LSP_HIP(launch_interp_partial(lde, (uint32_t)w, h, inv_z, GEN, tabN, L1N, logN, partial, &nb, st));
-        LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)w, sums, st));
-        LSP_HIP(launch_interp_partial(lde, (uint32_t)w, h, inv_zn, GEN, tabN, L1N, logN, partial, &nb, st));
-        LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)w, sums + w, st));
-        LSP_HIP(launch_interp_partial(qlde, (uint32_t)q, h, inv_z, GEN, tabN, L1N, logN, partial, &nb, st));
-        LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)q, sums + 2 * w, st));
+        if (g == 0) {
+            Fr* partial = ctx->fbuf("o_partial", ((h + 1023) / 1024) * maxw);
+            uint32_t nb = 0;
+            LSP_HIP(launch_interp_partial(lde, (uint32_t)w, h, inv_z, GEN, tabN, L1N, logN, partial, &nb, st));
+            LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)w, sums, st));
+            LSP_HIP(launch_interp_partial(lde, (uint32_t)w, h, inv_zn, GEN, tabN, L1N, logN, partial, &nb, st));
+            LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)w, sums + w, st));
+            LSP_HIP(launch_interp_partial(qlde, (uint32_t)q, h, inv_z, GEN, tabN, L1N, logN, partial, &nb, st));
+            LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)q, sums + 2 * w, st));
+        }
+        if (G > 1) comm.bcast(ctx, sums, (2 * w + q) * sizeof(Fr), 0);
         std::vector<Fr> hs(2 * w + q);
         LSP_HIP(hipMemcpyAsync(hs.data(), sums, hs.size() * sizeof(Fr), hipMemcpyDeviceToHost, st));
         LSP_HIP(hipStreamSynchronize(st));
@@ -348,8 +407,8 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
         Fr* dapw = ctx->fbuf("o_apw", apw.size() + q);
         LSP_HIP(hipMemcpyAsync(dapw, apw.data(), apw.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
         LSP_HIP(hipMemcpyAsync(dapw + apw.size(), proof->qc.data(), q * sizeof(Fr), hipMemcpyHostToDevice, st));
-        // FRI vectors: round r input of length N >> r, stored back to back
-        Fr* fvec = ctx->fbuf("f_vec", 2 * N);
+        // FRI vectors: this rank's slice of round r's input (length (N >> r) / G), back to back
+        Fr* fvec = ctx->fbuf("f_vec", 2 * S);
         ReduceArgs ra;
         ra.lde = lde;
         ra.w = (uint32_t)w;
@@ -362,7 +421,7 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
         ra.ry_zn = ry_zn;
         ra.ryq = dapw + apw.size();
         ra.out = fvec;
-        ra.n = N;
+        ra.n = S;
         LSP_HIP(launch_reduce_rows(ra, st));
         LSP_HIP(hipStreamSynchronize(st));  // apw/qc host vectors
         T.end("reduce rows");
@@ -371,15 +430,40 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
         T.begin("FRI prover");
         T.begin("commit phase");
         const size_t final_len = (size_t)1 << (lb + ctx->log_final_poly_len);
-        std::vector<size_t> voff, toff;
-        Fr* ftree = ctx->fbuf("f_tree", 2 * N);
+        struct FriRound {
+            const Fr* vec;   // this rank's copy of the round's input (its slice when sharded)
+            const Fr* tree;  // layers of this rank's (sub)tree
+            size_t ml;       // leaves of that (sub)tree
+            bool sharded;
+            std::vector<std::vector<Fr>> top;
+        };
+        std::vector<FriRound> rounds;
+        // shortest slice worth a collective per round (tests lower it to shard every round)
+        size_t FRI_SHARD_MIN = (size_t)1 << 12;
+        if (const char* e = std::getenv("LSP_FRI_SHARD_MIN")) FRI_SHARD_MIN = std::max<size_t>(1, std::strtoull(e, nullptr, 10));
+        Fr* ftree = ctx->fbuf("f_tree", 2 * S + 2 * (size_t)G * FRI_SHARD_MIN);
+        Fr* fv = fvec;
         size_t len = N, vo = 0, to = 0;
+        bool sharded = G > 1;
         const Fr half = fr_inv(fr_from_u64(2));
+        auto replicate = [&]() {  // gather the short vector to every rank
+            const size_t loc = len >> b;
+            Fr* rep = ctx->fbuf("f_rep", 2 * len);
+            comm.allgather(ctx, fv + vo, rep, loc * sizeof(Fr));
+            fv = rep;
+            vo = 0;
+            sharded = false;
+        };
         while (len > final_len) {
-            const size_t m = len / 2;
-            voff.push_back(vo);
-            toff.push_back(to);
-            const Fr root = commit_device(ctx, one_mat(fvec + vo, 2), m, ftree + to);
+            if (sharded && (len >> b) < 2 * FRI_SHARD_MIN) replicate();
+            const size_t m = len / 2, ml = sharded ? (m >> b) : m;
+            FriRound R;
+            R.vec = fv + vo;
+            R.tree = ftree + to;
+            R.ml = ml;
+            R.sharded = sharded;
+            const Fr lroot = commit_device(ctx, one_mat(fv + vo, 2), ml, ftree + to);
+            const Fr root = sharded ? shard_root(ctx, comm, lroot, R.top) : lroot;
             proof->roots.push_back(root);
             ch.observe(root);
             const Fr beta = ch.sample();
@@ -387,13 +471,16 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
             const uint32_t logm = log2_exact(m);
             const Fr ginv = fr_inv(host_two_adic_generator(logm + 1));
             const Fr* tabF = pow_table(ctx, "tabF", ginv, logm, L1F);
-            LSP_HIP(launch_fri_fold(fvec + vo, m, half, fr_mul(beta, half), tabF, L1F, fvec + vo + len, st));
-            vo += len;
-            to += 2 * m - 1;
+            LSP_HIP(launch_fri_fold(fv + vo, ml, half, fr_mul(beta, half), tabF, L1F, fv + vo + 2 * ml, st,
+                                    sharded ? (uint64_t)g * ml : 0, (int)logm));
+            rounds.push_back(std::move(R));
+            vo += 2 * ml;
+            to += 2 * ml - 1;
             len = m;
         }
+        if (sharded) replicate();
         std::vector<Fr> fin(len);
-        LSP_HIP(hipMemcpyAsync(fin.data(), fvec + vo, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
+        LSP_HIP(hipMemcpyAsync(fin.data(), fv + vo, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
         LSP_HIP(hipStreamSynchronize(st));
         T.end("commit phase");
         {
@@ -424,67 +511,82 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
         proof->pow_w = fr_from_u64(grind_device(ctx, ch, ctx->pow_bits));
         T.end("grind for proof-of-work witness");
 
-        // ---- query phase: one gather for every opened element
+        // ---- query phase: the owner of a query's row (rank idx / S) gathers the
+        // openings below the rank subtrees in one kernel; the layers above come
+        // from the host top trees every rank holds.
         T.begin("query phase");
-        const uint32_t nr = (uint32_t)proof->roots.size();
+        const uint32_t nr = (uint32_t)rounds.size();
+        const uint32_t nq = ctx->num_queries;
+        std::vector<size_t> idxs(nq);
+        for (uint32_t qi = 0; qi < nq; ++qi) idxs[qi] = (size_t)ch.sample_bits(logN);
+        size_t E = w + logS + q + logS;  // elements per query below the rank subtrees
+        for (const FriRound& R : rounds) E += 1 + log2_exact(R.ml);
         std::vector<uint64_t> ptrs;
-        std::vector<size_t> idxs(ctx->num_queries);
-        for (uint32_t qi = 0; qi < ctx->num_queries; ++qi) {
-            const size_t idx = (size_t)ch.sample_bits(logN);
-            idxs[qi] = idx;
+        std::vector<uint32_t> mine;
+        for (uint32_t qi = 0; qi < nq; ++qi) {
+            const size_t idx = idxs[qi];
+            if ((idx >> logS) != g) continue;
+            mine.push_back(qi);
+            const size_t li = idx - row0;
             auto P = [&](const Fr* p) { ptrs.push_back((uint64_t)(uintptr_t)p); };
-            for (size_t c = 0; c < w; ++c) P(lde + idx * w + c);
-            {
-                size_t off = 0, ln = N;
-                for (uint32_t i = 0; i < logN; ++i) {
-                    P(tlay + off + ((idx >> i) ^ 1));
+            auto path = [&](const Fr* lay, size_t leaves, size_t leaf) {
+                size_t off = 0, ln = leaves;
+                for (uint32_t i = 0; (1ull << i) < leaves; ++i) {
+                    P(lay + off + ((leaf >> i) ^ 1));
                     off += ln;
                     ln >>= 1;
                 }
-            }
-            for (size_t j = 0; j < q; ++j) P(qlde + idx * q + j);
-            {
-                size_t off = 0, ln = N;
-                for (uint32_t i = 0; i < logN; ++i) {
-                    P(qlay + off + ((idx >> i) ^ 1));
-                    off += ln;
-                    ln >>= 1;
-                }
-            }
-            size_t l2 = N;
+            };
+            for (size_t c = 0; c < w; ++c) P(lde + li * w + c);
+            path(tlay, S, li);
+            for (size_t j = 0; j < q; ++j) P(qlde + li * q + j);
+            path(qlay, S, li);
             for (uint32_t r = 0; r < nr; ++r) {
-                const size_t m = l2 / 2, ii = idx >> r, pair = ii >> 1;
-                P(fvec + voff[r] + (ii ^ 1));
-                size_t off = toff[r], ln = m;
-                const uint32_t lg = log2_exact(m);
-                for (uint32_t i = 0; i < lg; ++i) {
-                    P(ftree + off + ((pair >> i) ^ 1));
-                    off += ln;
-                    ln >>= 1;
-                }
-                l2 = m;
+                const FriRound& R = rounds[r];
+                const size_t ii = idx >> r;                           // global index in round r's vector
+                const size_t base = R.sharded ? (size_t)g * 2 * R.ml : 0;  // global index of R.vec[0]
+                P(R.vec + ((ii ^ 1) - base));
+                path(R.tree, R.ml, (ii >> 1) - base / 2);
             }
         }
-        uint64_t* dptrs = (uint64_t*)ctx->buf("g_ptrs", ptrs.size() * sizeof(uint64_t));
-        Fr* dgot = ctx->fbuf("g_out", ptrs.size());
-        LSP_HIP(hipMemcpyAsync(dptrs, ptrs.data(), ptrs.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-        LSP_HIP(launch_gather(dptrs, dgot, ptrs.size(), st));
-        std::vector<Fr> got(ptrs.size());
-        LSP_HIP(hipMemcpyAsync(got.data(), dgot, got.size() * sizeof(Fr), hipMemcpyDeviceToHost, st));
-        LSP_HIP(hipStreamSynchronize(st));
-        size_t cur = 0;
-        for (uint32_t qi = 0; qi < ctx->num_queries; ++qi) {
+        LSP_REQUIRE(ptrs.size() == mine.size() * E, LSP_E_STATE, "query opening layout mismatch");
+        std::vector<Fr> slots((size_t)nq * E, fr_zero());
+        if (!ptrs.empty()) {
+            uint64_t* dptrs = (uint64_t*)ctx->buf("g_ptrs", ptrs.size() * sizeof(uint64_t));
+            Fr* dgot = ctx->fbuf("g_out", ptrs.size());
+            LSP_HIP(hipMemcpyAsync(dptrs, ptrs.data(), ptrs.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+            LSP_HIP(launch_gather(dptrs, dgot, ptrs.size(), st));
+            std::vector<Fr> got(ptrs.size());
+            LSP_HIP(hipMemcpyAsync(got.data(), dgot, got.size() * sizeof(Fr), hipMemcpyDeviceToHost, st));
+            LSP_HIP(hipStreamSynchronize(st));
+            for (size_t k = 0; k < mine.size(); ++k)
+                std::copy(got.begin() + k * E, got.begin() + (k + 1) * E, slots.begin() + (size_t)mine[k] * E);
+        }
+        const std::vector<Fr> all = G > 1 ? comm.allgather_fr(ctx, slots.data(), slots.size()) : slots;
+        auto top_path = [&](const std::vector<std::vector<Fr>>& top, size_t sub, std::vector<Fr>& out) {
+            for (uint32_t i = 0; i + 1 < top.size(); ++i) out.push_back(top[i][(sub >> i) ^ 1]);
+        };
+        for (uint32_t qi = 0; qi < nq; ++qi) {
+            const size_t idx = idxs[qi], o = idx >> logS;
+            const Fr* e = all.data() + (o * nq + qi) * E;
             lsp_query qq;
-            qq.trow.assign(got.begin() + cur, got.begin() + cur + w);
-            cur += w;
-            tree_path(got, cur, logN, qq.tpath);
-            qq.qrow.assign(got.begin() + cur, got.begin() + cur + q);
-            cur += q;
-            tree_path(got, cur, logN, qq.qpath);
+            qq.trow.assign(e, e + w);
+            e += w;
+            qq.tpath.assign(e, e + logS);
+            e += logS;
+            top_path(ttop, o, qq.tpath);
+            qq.qrow.assign(e, e + q);
+            e += q;
+            qq.qpath.assign(e, e + logS);
+            e += logS;
+            top_path(qtop, o, qq.qpath);
             for (uint32_t r = 0; r < nr; ++r) {
-                qq.sib.push_back(got[cur++]);
-                std::vector<Fr> pth;
-                tree_path(got, cur, logN - r - 1, pth);
+                const FriRound& R = rounds[r];
+                qq.sib.push_back(*e++);
+                const uint32_t lg = log2_exact(R.ml);
+                std::vector<Fr> pth(e, e + lg);
+                e += lg;
+                if (R.sharded) top_path(R.top, o, pth);
                 qq.fpath.push_back(std::move(pth));
             }
             proof->queries.push_back(std::move(qq));
@@ -499,6 +601,12 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
         throw;
     }
     return proof;
+}
+
+lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, const Air& air, const Fr* pub,
+                        size_t npub) {
+    SoloComm solo;
+    return prove_shard(ctx, solo, d_trace, h, w, air, pub, npub);
 }
 
 // --------------------------------------------------------- serialization

@@ -4,13 +4,19 @@
 #include "host.hpp"
 
 namespace lsp {
-// coset LDE of an h x w device matrix with per-column shifts -> (h << added_bits) x w bit-reversed rows
+// coset LDE of an h x w device matrix with per-column shifts -> (h << added_bits) x w bit-reversed rows;
+// with nk > 0 only the coset blocks [k0, k0 + nk) (rows k0*h .. (k0+nk)*h - 1 of the full result)
 void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added_bits, const Fr* shifts_host,
-                Fr* d_out);
+                Fr* d_out, uint32_t k0 = 0, uint32_t nk = 0);
 // leaves + every layer into `layers` (2*height - 1); returns the root
 Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers);
 lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, const Air& air, const Fr* pub,
                         size_t npub);
+struct Comm;
+// one rank of a proof sharded over comm.size ranks (prove_device = 1 rank);
+// every rank returns the same proof
+lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, size_t w, const Air& air,
+                       const Fr* pub, size_t npub);
 std::vector<uint8_t> serialize(const lsp_proof& p);
 // 0 = accept, otherwise the failing check (host CPU verifier)
 int verify_host(const lsp_ctx* ctx, const Air& air, const Fr* pub, size_t npub, const uint8_t* b, size_t n);

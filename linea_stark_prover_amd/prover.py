@@ -59,6 +59,18 @@ class StarkConfig:
         return a, d, rc
 
 
+def _take_proof(proof: ctypes.c_void_p) -> bytes:
+    """serialize and free an lsp_proof handle"""
+    try:
+        n = ctypes.c_size_t()
+        L.check(L.lib().lsp_proof_serialize(proof, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value)
+        L.check(L.lib().lsp_proof_serialize(proof, buf, n.value, ctypes.byref(n)))
+        return buf.raw[:n.value]
+    finally:
+        L.lib().lsp_proof_free(proof)
+
+
 class Context:
     """One lsp_ctx: a GPU, a stream, the Poseidon2 constants and a buffer pool."""
 
@@ -186,14 +198,7 @@ class Context:
             t = _fr_arr(trace)
             self._chk(L.lib().lsp_prove(self.h, _ptr(t), t.shape[0], t.shape[1], desc, len(desc), _ptr(pub),
                                         pub.shape[0], L.LSP_MEM_HOST, ctypes.byref(proof)))
-        try:
-            n = ctypes.c_size_t()
-            L.check(L.lib().lsp_proof_serialize(proof, None, 0, ctypes.byref(n)))
-            buf = ctypes.create_string_buffer(n.value)
-            L.check(L.lib().lsp_proof_serialize(proof, buf, n.value, ctypes.byref(n)))
-            return buf.raw[:n.value]
-        finally:
-            L.lib().lsp_proof_free(proof)
+        return _take_proof(proof)
 
     def verify(self, proof: bytes, air: LineaAIR, public_values: np.ndarray) -> bool:
         desc = (ctypes.c_int32 * len(air.descriptor()))(*air.descriptor())
@@ -327,6 +332,50 @@ def gen_wide_trace(log_n: int, alpha: np.ndarray, delta: np.ndarray, nlookup: in
     L.check(L.lib().lsp_gen_wide_trace(*args, _ptr(rows), rows.shape[0] * w.value, desc, dl.value, ctypes.byref(w),
                                        ctypes.byref(dl)))
     return rows, LineaAIR.from_descriptor(list(desc))
+
+
+class ProverGroup:
+    """G = 2^b contexts proving one proof together (lsp_prove_group, SURVEY
+    8(e)): distinct devices of one host, or one device repeated as virtual
+    ranks.  The proof is byte-identical to Context.prove's."""
+
+    def __init__(self, contexts: Sequence[Context]):
+        self.contexts = list(contexts)
+        arr = (ctypes.c_void_p * len(self.contexts))(*[c.h.value for c in self.contexts])
+        g = ctypes.c_void_p()
+        L.check(L.lib().lsp_group_create(arr, len(self.contexts), ctypes.byref(g)))
+        self.h = g
+
+    def close(self):
+        if self.h:
+            L.lib().lsp_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def prove(self, traces, air: LineaAIR, public_values: np.ndarray, h: Optional[int] = None,
+              w: Optional[int] = None) -> bytes:
+        """`traces`: one (h, w, 4) host array (every rank copies it), or a list of
+        per-rank device pointers (ints) with h and w given."""
+        desc = (ctypes.c_int32 * len(air.descriptor()))(*air.descriptor())
+        pub = _fr_arr(public_values).reshape(-1, 4)
+        G = len(self.contexts)
+        proof = ctypes.c_void_p()
+        if isinstance(traces, (list, tuple)):
+            ptrs = (ctypes.c_void_p * G)(*traces)
+            mem = L.LSP_MEM_DEVICE
+        else:
+            t = _fr_arr(traces)
+            h, w = t.shape[0], t.shape[1]
+            ptrs = (ctypes.c_void_p * G)(*([t.ctypes.data] * G))
+            mem = L.LSP_MEM_HOST
+        L.check(L.lib().lsp_prove_group(self.h, ptrs, h, w, desc, len(desc), _ptr(pub), pub.shape[0], mem,
+                                        ctypes.byref(proof)), self.contexts[0].h)
+        return _take_proof(proof)
 
 
 def prove(config: StarkConfig, air: LineaAIR, trace: np.ndarray, public_values: np.ndarray,

@@ -1,0 +1,87 @@
+"""Sharded prove (lsp_prove_group): G = 2, 4, 8 ranks as virtual
+ranks on one GPU (one context and one host thread each, exchanges through
+device copies).  The proof must be byte-identical to the single-rank proof,
+which the parity tests pin to the oracle."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _group(ctx, G):
+    from linea_stark_prover_amd.prover import Context, ProverGroup
+    ctxs = [Context(ctx.config) for _ in range(G)]
+    return ProverGroup(ctxs), ctxs
+
+
+@pytest.mark.parametrize("G", [2, 4, 8])
+@pytest.mark.parametrize("log_n,ncols", [(3, 3), (9, 3), (10, 6)])
+@pytest.mark.parametrize("fri_min", [None, "2"])
+def test_group_proof_equals_single(gpu_ctx, monkeypatch, G, log_n, ncols, fri_min):
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import gen_permutation_trace
+    if fri_min:
+        monkeypatch.setenv("LSP_FRI_SHARD_MIN", fri_min)  # shard the FRI rounds down to 4-element slices
+    a, d, _ = gpu_ctx.config.seeded()
+    tr = gen_permutation_trace(log_n, ncols, a, d)
+    pub = np.concatenate([a, d])
+    air = permutation_air(ncols)
+    single = gpu_ctx.prove(tr, air, pub)
+    grp, _ = _group(gpu_ctx, G)
+    got = grp.prove(tr, air, pub)
+    assert got == single
+    assert gpu_ctx.verify(got, air, pub)
+
+
+def test_group_matches_oracle(gpu_ctx, oracle_lib, monkeypatch):
+    from linea_stark_prover_amd.air import permutation_air
+    monkeypatch.setenv("LSP_FRI_SHARD_MIN", "8")
+    p = oracle_lib.setup()
+    tb, w = oracle_lib.gen_perm_trace(p, 8, 3)
+    tr = np.frombuffer(tb.raw, dtype=np.uint64).reshape(1 << 8, w, 4).copy()
+    pub = np.concatenate([np.array(p.alpha, np.uint64).reshape(1, 4), np.array(p.delta, np.uint64).reshape(1, 4)])
+    grp, _ = _group(gpu_ctx, 4)
+    got = grp.prove(tr, permutation_air(3), pub)
+    exp = oracle_lib.prove(p, tr.ctypes.data, 1 << 8, w, oracle_lib.perm_air(3))
+    assert got == exp
+
+
+@pytest.mark.parametrize("G", [2, 8])
+def test_group_wide_air(gpu_ctx, monkeypatch, G):
+    """lookup + permutation configs, q = 8 for the 6+6 groups: with G = 8 every
+    rank owns one quotient chunk"""
+    from linea_stark_prover_amd.prover import gen_wide_trace
+    monkeypatch.setenv("LSP_FRI_SHARD_MIN", "4")
+    a, d, _ = gpu_ctx.config.seeded()
+    tr, air = gen_wide_trace(7, a, d, 2, 3, 2, 3, 6)
+    pub = np.concatenate([a, d])
+    single = gpu_ctx.prove(tr, air, pub)
+    grp, _ = _group(gpu_ctx, G)
+    assert grp.prove(tr, air, pub) == single
+
+
+def test_group_device_resident_traces(gpu_ctx):
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import gen_permutation_trace
+    a, d, _ = gpu_ctx.config.seeded()
+    tr = gen_permutation_trace(12, 3, a, d)
+    pub = np.concatenate([a, d])
+    grp, ctxs = _group(gpu_ctx, 2)
+    ptrs = []
+    for c in ctxs:
+        p = c.dev_alloc(tr.nbytes)
+        c.h2d(p, tr)
+        ptrs.append(p)
+    got = grp.prove(ptrs, permutation_air(3), pub, tr.shape[0], tr.shape[1])
+    assert got == gpu_ctx.prove(tr, permutation_air(3), pub)
+
+
+def test_group_rejects_too_many_ranks(gpu_ctx):
+    """G > blowup (16 > 8) cannot own whole cosets: a clean error on every rank"""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import gen_permutation_trace
+    a, d, _ = gpu_ctx.config.seeded()
+    tr = gen_permutation_trace(5, 3, a, d)
+    grp, _ = _group(gpu_ctx, 16)
+    with pytest.raises(RuntimeError, match="at most 2\\^log_blowup"):
+        grp.prove(tr, permutation_air(3), np.concatenate([a, d]))

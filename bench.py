@@ -10,6 +10,13 @@ the host.  For N > 1 (launched by torch.distributed.run) every rank proves its
 own independent trace (SURVEY 8(d) C5, replicas, no data-path collective);
 ``value`` = all rows proven by all ranks / the max-over-ranks wall time.
 
+``--shard``: the N ranks prove ONE trace together
+(lsp_prove_sharded; rank g owns LDE rows [g N/G, (g+1) N/G)), exchanging
+subtree roots, quotient chunks, opened values and query openings over RCCL
+(``--comm rccl``, device-direct over xGMI) or a gloo group (``--comm gloo``,
+host-staged; lets several ranks share one GPU).  ``value`` = rows of the one
+proof / max-over-ranks wall time ("scaling": "strong").
+
 Besides the contract fields the JSON line carries:
   roofline       the coset LDE (the metric's "NTT HBM GB/s"): algorithmic
                  bytes 32*w*(h + N) per coset_lde_batch / its event-timed
@@ -49,6 +56,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=0x4C494E4541)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-log-n", type=int, default=17, help="bounded CPU-baseline sample size")
+    ap.add_argument("--shard", action="store_true", help="one proof sharded over the N ranks (C4)")
+    ap.add_argument("--comm", choices=["rccl", "gloo"], default="rccl", help="--shard exchange transport")
+    ap.add_argument("--device", type=int, default=None, help="GPU of this rank (default: LOCAL_RANK)")
+    ap.add_argument("--dump-proof", default=None, help="rank 0 writes the last proof here")
     return ap.parse_args()
 
 
@@ -63,16 +74,25 @@ def main():
     from linea_stark_prover_amd.air import permutation_air
     from linea_stark_prover_amd.prover import Context, StarkConfig, gen_permutation_trace, gen_wide_trace
 
+    shard = args.shard
+    if shard:
+        from linea_stark_prover_amd import shard as S  # imports torch before the HIP library loads
     cfg = StarkConfig(seed=args.seed)
-    ctx = Context(cfg, device=local)
+    ctx = Context(cfg, device=local if args.device is None else args.device)
+    if shard:
+        if args.comm == "rccl":
+            S.attach_rccl(ctx)
+        else:
+            S.GlooComm().attach(ctx)
     a, d, _ = cfg.seeded()
     pub = np.concatenate([a, d])
     h = 1 << args.log_n
+    tseed = args.seed if shard else rank_seed(args.seed, rank)  # sharded: every rank holds the same trace
     if args.air == "wide":
-        trace, air = gen_wide_trace(args.log_n, a, d, seed=rank_seed(args.seed, rank))
+        trace, air = gen_wide_trace(args.log_n, a, d, seed=tseed)
     else:
         air = permutation_air(args.ncols)
-        trace = gen_permutation_trace(args.log_n, args.ncols, a, d, seed=rank_seed(args.seed, rank))
+        trace = gen_permutation_trace(args.log_n, args.ncols, a, d, seed=tseed)
     w = trace.shape[1]
     dtrace = ctx.dev_alloc(trace.nbytes)
     ctx.h2d(dtrace, trace)  # resident in HBM before the timed region
@@ -83,14 +103,20 @@ def main():
         for name, ms in ctx.last_timings():
             phases_acc[name] = phases_acc.get(name, 0.0) + ms
 
-    elapsed, proof = timed_steps(lambda: ctx.prove(dtrace, air, pub, h, w), args.steps, args.warmup, dist,
-                                 sync=ctx.synchronize, on_step=record)
+    if shard:
+        step = lambda: S.prove_sharded(ctx, dtrace, air, pub, h, w)  # noqa: E731
+    else:
+        step = lambda: ctx.prove(dtrace, air, pub, h, w)  # noqa: E731
+    elapsed, proof = timed_steps(step, args.steps, args.warmup, dist, sync=ctx.synchronize, on_step=record)
     phases = {k: v / max(args.steps, 1) for k, v in phases_acc.items()}
     verified = ctx.verify(proof, air, pub) if proof is not None else False
 
+    if rank == 0 and args.dump_proof and proof is not None:
+        with open(args.dump_proof, "wb") as f:
+            f.write(proof)
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
-        value = world * h * args.steps / elapsed
+        value = (1 if shard else world) * h * args.steps / elapsed
         N = h << cfg.log_blowup
         import ctypes
         from linea_stark_prover_amd import _lib
@@ -99,16 +125,11 @@ def main():
         _lib.check(_lib.lib().lsp_log_quotient_degree(desc, len(desc), cfg.public_degree, ctypes.byref(lq)))
         q = 1 << lq.value
         lde_ms = phases.get("coset_lde_batch", float("nan"))
-        lde_bytes = 32 * w * (h + N)
+        Nr = N // world if shard else N  # LDE rows (Merkle leaves) this rank computes
+        lde_bytes = 32 * w * (h + Nr)
         achieved = lde_bytes / (lde_ms * 1e-3) / 1e9
-        # Poseidon2 Merkle work of one proof (SURVEY 8(d) perm-count formula)
-        perms = N * ((w + 1) // 2) + (N - 1) + N * ((q + 1) // 2) + (N - 1)
-        L = N
-        while L > (1 << cfg.log_blowup):
-            perms += L // 2 + (L // 2 - 1)
-            L //= 2
         merkle_ms = phases.get("merkle tree", float("nan"))
-        trace_perms = N * ((w + 1) // 2) + (N - 1)
+        trace_perms = Nr * ((w + 1) // 2) + (Nr - 1)
         mul_per_perm = 230
         calib = ctx.calibrate_fr_mul() if hasattr(ctx, "calibrate_fr_mul") else None
         valu_achieved = trace_perms * mul_per_perm / (merkle_ms * 1e-3) / 1e9
@@ -122,18 +143,19 @@ def main():
             "ms_per_step": ms_per_step,
             "prove_time_s": ms_per_step / 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if shard else "weak",
             "vs_baseline": value / PUBLISHED_ROWS_PER_S,
             "baseline_published": {"value": PUBLISHED_ROWS_PER_S, "unit": "trace-rows/s",
                                    "source": "reference README.md:11, ~330 s for 2^19 rows on a 16-core CPU"},
             "dtype": "fr253 (BLS12-377 Fr, 8x u32 Montgomery limbs)",
-            "data": "synthetic (seeded permutation trace, SURVEY 8(d) C1)",
+            "data": "synthetic (seeded permutation trace, SURVEY 8(d) " + ("C4)" if shard else "C1)"),
             "config": {"workload": (f"{args.ncols}x{args.ncols} permutation AIR" if args.air == "perm" else
                                     "wide AIR (4 LogUp lookups + 8 permutation groups of 6+6)") +
                                    f", 2^{args.log_n} rows (w={w}, q={q} quotient chunks, log_blowup "
                                    f"{cfg.log_blowup}, {cfg.num_queries} queries, Poseidon2-w3 Merkle, FRI)",
                        "log_n": args.log_n, "width": w, "fri_queries": cfg.num_queries,
-                       "parallelism": "replicas" if world > 1 else "single-gpu"},
+                       "parallelism": (f"sharded{world} ({args.comm})" if shard else
+                                       "replicas" if world > 1 else "single-gpu")},
             "verified": bool(verified),
             "phases_ms": {k: round(v, 3) for k, v in phases.items()},
             "roofline": {"bound": "hbm", "kernel": "coset_lde_batch (trace, w x 2^log_n -> 8x)",

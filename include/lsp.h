@@ -196,6 +196,30 @@ int lsp_group_create(lsp_ctx *const *ctxs, int n, lsp_group **out);
 int lsp_group_destroy(lsp_group *grp);
 int lsp_prove_group(lsp_group *grp, const lsp_fr *const *traces, size_t h, size_t w, const int32_t *air,
                     size_t air_len, const lsp_fr *public_values, size_t npub, int mem, lsp_proof **out);
+/* Process-per-GPU sharding: each of the G processes attaches a communicator
+ * to its context (rank g of G), then all call lsp_prove_sharded together;
+ * ranks, data layout and result are those of lsp_prove_group.
+ *   lsp_comm_ops   the caller's transport over host buffers (allgather: recv
+ *                  receives size * bytes in rank order; bcast: root's buf to
+ *                  every rank); callbacks return 0 on success.
+ *   RCCL           device-direct over xGMI: rank 0 creates the id with
+ *                  lsp_comm_rccl_unique_id, the caller distributes its 128
+ *                  bytes, every rank calls lsp_ctx_attach_rccl (collective). */
+typedef struct lsp_comm_ops {
+    int rank, size;
+    void *user;
+    int (*allgather)(void *user, const void *send, void *recv, size_t bytes);
+    int (*bcast)(void *user, void *buf, size_t bytes, int root);
+} lsp_comm_ops;
+int lsp_ctx_attach_comm_ops(lsp_ctx *ctx, const lsp_comm_ops *ops);
+int lsp_comm_rccl_unique_id(uint8_t id[128]);
+int lsp_ctx_attach_rccl(lsp_ctx *ctx, const uint8_t id[128], int rank, int size);
+int lsp_ctx_detach_comm(lsp_ctx *ctx);
+/* collective check of the attached communicator: an allgather and a
+ * broadcast of known patterns (LSP_E_STATE on wrong data) */
+int lsp_comm_selftest(lsp_ctx *ctx);
+int lsp_prove_sharded(lsp_ctx *ctx, const lsp_fr *trace, size_t h, size_t w, const int32_t *air, size_t air_len,
+                      const lsp_fr *public_values, size_t npub, int mem, lsp_proof **out);
 /* serialized proof (format in DESIGN.md); buf == NULL -> *len = required size */
 int lsp_proof_serialize(const lsp_proof *proof, uint8_t *buf, size_t cap, size_t *len);
 int lsp_proof_free(lsp_proof *proof);

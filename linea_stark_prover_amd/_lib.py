@@ -26,6 +26,15 @@ class LspParams(ctypes.Structure):
                 ("proof_of_work_bits", ctypes.c_uint32), ("public_degree", ctypes.c_int32)]
 
 
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+BCAST_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
+
+
+class LspCommOps(ctypes.Structure):
+    _fields_ = [("rank", ctypes.c_int), ("size", ctypes.c_int), ("user", ctypes.c_void_p),
+                ("allgather", ALLGATHER_FN), ("bcast", BCAST_FN)]
+
+
 class LspError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"lsp error {code}: {msg}")
@@ -82,6 +91,14 @@ _SIGS = {
     "lsp_proof_serialize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                            ctypes.POINTER(ctypes.c_size_t)]),
     "lsp_proof_free": (ctypes.c_int, [ctypes.c_void_p]),
+    "lsp_ctx_attach_comm_ops": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(LspCommOps)]),
+    "lsp_comm_rccl_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "lsp_ctx_attach_rccl": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "lsp_ctx_detach_comm": (ctypes.c_int, [ctypes.c_void_p]),
+    "lsp_comm_selftest": (ctypes.c_int, [ctypes.c_void_p]),
+    "lsp_prove_sharded": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
+                                         ctypes.c_size_t, c_fr_p, ctypes.c_size_t, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_void_p)]),
     "lsp_group_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
                                         ctypes.POINTER(ctypes.c_void_p)]),
     "lsp_group_destroy": (ctypes.c_int, [ctypes.c_void_p]),

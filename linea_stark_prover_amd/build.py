@@ -25,7 +25,7 @@ ARCH = os.environ.get("LSP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["k_ntt.hip", "k_hash.hip", "k_field.hip", "k_quotient.hip", "k_open.hip",
-           "host.cpp", "prove.cpp", "verify.cpp", "witness.cpp", "capi.cpp"]
+           "host.cpp", "prove.cpp", "verify.cpp", "witness.cpp", "comm_ext.cpp", "capi.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
           "-Wno-unused-variable", "-I", os.path.join(ROOT, "include")]
 
@@ -71,7 +71,7 @@ def build(force: bool = False, jobs: int = None, verbose: bool = True) -> str:
         with cf.ThreadPoolExecutor(jobs) as ex:
             list(ex.map(_compile, todo))
     if todo or _stale(LIB, objs):
-        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs + ["-lpthread"]
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs + ["-lpthread", "-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

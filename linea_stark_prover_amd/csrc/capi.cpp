@@ -176,6 +176,8 @@ int lsp_ctx_create(int device, const lsp_params* p, lsp_ctx** out) {
 
 int lsp_ctx_destroy(lsp_ctx* ctx) {
     if (!ctx) return LSP_OK;
+    delete ctx->comm;
+    ctx->comm = nullptr;
     if (ctx->device == LSP_HOST_ONLY) {
         delete ctx;
         return LSP_OK;
@@ -629,6 +631,86 @@ int lsp_prove_group(lsp_group* grp, const lsp_fr* const* traces, size_t h, size_
         for (int r = (bad < 0 ? 1 : 0); r < G; ++r) delete res[r];
         if (bad >= 0) throw LspError(code[bad], "rank " + std::to_string(bad) + ": " + msg[bad]);
         *out = res[0];
+    });
+}
+
+int lsp_ctx_attach_comm_ops(lsp_ctx* ctx, const lsp_comm_ops* ops) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && ops && ops->allgather && ops->bcast, LSP_E_ARG, "bad communicator");
+        LSP_REQUIRE(ops->size >= 1 && ops->rank >= 0 && ops->rank < ops->size, LSP_E_ARG, "bad rank / size");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        delete ctx->comm;
+        ctx->comm = make_callback_comm(*ops);
+    });
+}
+
+int lsp_comm_rccl_unique_id(uint8_t id[128]) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(id, LSP_E_ARG, "null id");
+        rccl_unique_id(id);
+    });
+}
+
+int lsp_ctx_attach_rccl(lsp_ctx* ctx, const uint8_t id[128], int rank, int size) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && id && size >= 1 && rank >= 0 && rank < size, LSP_E_ARG, "bad RCCL attach arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        delete ctx->comm;
+        ctx->comm = nullptr;
+        ctx->comm = make_rccl_comm(id, rank, size);
+    });
+}
+
+int lsp_comm_selftest(lsp_ctx* ctx) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx, LSP_E_ARG, "null ctx");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        LSP_REQUIRE(ctx->comm, LSP_E_STATE, "no communicator attached");
+        need_gpu(ctx);
+        Comm& c = *ctx->comm;
+        const size_t n = 1000;  // words per rank, not a multiple of anything in particular
+        std::vector<uint32_t> mine(n), got(n * (size_t)c.size);
+        for (size_t i = 0; i < n; ++i) mine[i] = (uint32_t)(c.rank + 1) * 2654435761u + (uint32_t)i;
+        uint32_t* s = (uint32_t*)ctx->buf("selftest_s", n * 4);
+        uint32_t* r = (uint32_t*)ctx->buf("selftest_r", n * 4 * (size_t)c.size);
+        LSP_HIP(hipMemcpyAsync(s, mine.data(), n * 4, hipMemcpyHostToDevice, ctx->stream));
+        c.allgather(ctx, s, r, n * 4);
+        LSP_HIP(hipMemcpyAsync(got.data(), r, got.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+        LSP_HIP(hipStreamSynchronize(ctx->stream));
+        for (int k = 0; k < c.size; ++k)
+            for (size_t i = 0; i < n; ++i)
+                LSP_REQUIRE(got[k * n + i] == (uint32_t)(k + 1) * 2654435761u + (uint32_t)i, LSP_E_STATE,
+                            "communicator allgather returned wrong data");
+        c.bcast(ctx, s, n * 4, 0);
+        LSP_HIP(hipMemcpyAsync(got.data(), s, n * 4, hipMemcpyDeviceToHost, ctx->stream));
+        LSP_HIP(hipStreamSynchronize(ctx->stream));
+        for (size_t i = 0; i < n; ++i)
+            LSP_REQUIRE(got[i] == 2654435761u + (uint32_t)i, LSP_E_STATE, "communicator bcast returned wrong data");
+    });
+}
+
+int lsp_ctx_detach_comm(lsp_ctx* ctx) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx, LSP_E_ARG, "null ctx");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        delete ctx->comm;
+        ctx->comm = nullptr;
+    });
+}
+
+int lsp_prove_sharded(lsp_ctx* ctx, const lsp_fr* trace, size_t h, size_t w, const int32_t* air, size_t air_len,
+                      const lsp_fr* pubv, size_t npub, int mem, lsp_proof** out) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && out && pubv, LSP_E_ARG, "bad prove arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        LSP_REQUIRE(ctx->comm, LSP_E_STATE, "no communicator attached (lsp_ctx_attach_*)");
+        need_gpu(ctx);
+        const Air A = Air::parse(air, air_len);
+        std::vector<Fr> pub(npub);
+        for (size_t i = 0; i < npub; ++i) pub[i] = to_fr(pubv[i]);
+        const Fr* din = dev_in(ctx, trace, h * w, mem, "trace_in");
+        *out = prove_shard(ctx, *ctx->comm, din, h, w, A, pub.data(), npub);
     });
 }
 

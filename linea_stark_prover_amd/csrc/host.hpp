@@ -149,8 +149,13 @@ struct lsp_tree {
     std::vector<lsp::Fr*> mats;        // device copies (owned) of the committed matrices
 };
 
+namespace lsp {
+struct Comm;
+}
+
 struct lsp_ctx {
     int device = 0;
+    lsp::Comm* comm = nullptr;  // attached communicator of a process-per-GPU sharded prove (owned)
     hipStream_t stream = nullptr;
     lsp::P2Host p2;
     lsp::Fr* rc_dev = nullptr;    // round constants, ark form

@@ -18,6 +18,10 @@ struct Comm;
 lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, size_t w, const Air& air,
                        const Fr* pub, size_t npub);
 std::vector<uint8_t> serialize(const lsp_proof& p);
+// communicators of a process-per-GPU sharded prove (comm_ext.cpp)
+Comm* make_callback_comm(const lsp_comm_ops& ops);
+void rccl_unique_id(uint8_t out[128]);
+Comm* make_rccl_comm(const uint8_t id[128], int rank, int size);
 // 0 = accept, otherwise the failing check (host CPU verifier)
 int verify_host(const lsp_ctx* ctx, const Air& air, const Fr* pub, size_t npub, const uint8_t* b, size_t n);
 }  // namespace lsp

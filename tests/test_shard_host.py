@@ -1,0 +1,101 @@
+"""Host side of the process-per-GPU sharded prove (no GPU): the gloo
+transport behind lsp_comm_ops on a world_size-2 group, and the C-ABI's
+argument / state checks."""
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+WORKER = textwrap.dedent("""
+    import ctypes, json, os, sys
+    sys.path.insert(0, {root!r})
+    from linea_stark_prover_amd.replicas import init_from_env
+    d = init_from_env()
+    import numpy as np
+    from linea_stark_prover_amd.shard import GlooComm
+    c = GlooComm()
+    n = 37
+    mine = (np.arange(n, dtype=np.uint8) * 3 + 11 * (c.rank + 1)).astype(np.uint8)
+    recv = np.zeros(n * c.size, np.uint8)
+    # through the ctypes callback objects, as the C side calls them
+    rc1 = c.ops.allgather(None, mine.ctypes.data, recv.ctypes.data, n)
+    buf = mine.copy() if c.rank == 1 else np.zeros(n, np.uint8)
+    rc2 = c.ops.bcast(None, buf.ctypes.data, n, 1)
+    print(json.dumps({{"rank": c.rank, "rc": [rc1, rc2], "recv": recv.tolist(), "bcast": buf.tolist()}}), flush=True)
+    d.close()
+""")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_gloo_comm_ops_two_ranks(tmp_path, product_lib):
+    import json
+    script = tmp_path / "w.py"
+    script.write_text(WORKER.format(root=ROOT))
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=240)
+        assert p.returncode == 0, e
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    outs.sort(key=lambda x: x["rank"])
+    n = 37
+    exp = np.concatenate([(np.arange(n) * 3 + 11 * (r + 1)) % 256 for r in range(2)]).tolist()
+    for o in outs:
+        assert o["rc"] == [0, 0]
+        assert o["recv"] == exp
+        assert o["bcast"] == exp[n:]  # rank 1's pattern on every rank
+
+
+@pytest.fixture
+def host_ctx(product_lib):
+    from linea_stark_prover_amd.prover import Context, StarkConfig
+    return Context(StarkConfig(), device=-1)
+
+
+def test_prove_sharded_needs_a_communicator(host_ctx):
+    from linea_stark_prover_amd import _lib
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.shard import prove_sharded
+    tr = np.zeros((8, 8, 4), np.uint64)
+    with pytest.raises(_lib.LspError, match="no communicator"):
+        prove_sharded(host_ctx, tr, permutation_air(3), np.zeros((2, 4), np.uint64))
+
+
+def test_comm_ops_argument_checks(host_ctx):
+    import ctypes
+    from linea_stark_prover_amd import _lib as L
+    ag = L.ALLGATHER_FN(lambda *a: 0)
+    bc = L.BCAST_FN(lambda *a: 0)
+    bad = L.LspCommOps(2, 2, None, ag, bc)  # rank outside [0, size)
+    assert L.lib().lsp_ctx_attach_comm_ops(host_ctx.h, ctypes.byref(bad)) == L.LSP_E_ARG
+    ok = L.LspCommOps(0, 1, None, ag, bc)
+    assert L.lib().lsp_ctx_attach_comm_ops(host_ctx.h, ctypes.byref(ok)) == L.LSP_OK
+    # the self-test needs the GPU the host-only context does not have
+    assert L.lib().lsp_comm_selftest(host_ctx.h) == L.LSP_E_STATE
+    assert L.lib().lsp_ctx_detach_comm(host_ctx.h) == L.LSP_OK
+
+
+def test_group_needs_gpu_contexts(host_ctx):
+    from linea_stark_prover_amd import _lib
+    from linea_stark_prover_amd.prover import ProverGroup
+    with pytest.raises(_lib.LspError, match="GPU context"):
+        ProverGroup([host_ctx, host_ctx])

@@ -22,8 +22,8 @@ Besides the contract fields the JSON line carries:
                  bytes 32*w*(h + N) per coset_lde_batch / its event-timed
                  duration, vs the 8 TB/s HBM3E peak
   roofline_valu  the dominant kernel family (Poseidon2 Merkle hashing):
-                 algorithmic Fr multiplications / time vs the Fr-mul peak
-                 of the same multiplier measured by lsp_calibrate_fr_mul
+                 permutations / time vs the permutation rate of the same
+                 code on register-resident states (lsp_calibrate_poseidon2)
   cpu_baseline   the C restatement (oracle/, "port") proving a bounded
                  sample on the host cores, rank 0 at N = 1 only
 """
@@ -130,9 +130,8 @@ def main():
         achieved = lde_bytes / (lde_ms * 1e-3) / 1e9
         merkle_ms = phases.get("merkle tree", float("nan"))
         trace_perms = Nr * ((w + 1) // 2) + (Nr - 1)
-        mul_per_perm = 230
-        calib = ctx.calibrate_fr_mul() if hasattr(ctx, "calibrate_fr_mul") else None
-        valu_achieved = trace_perms * mul_per_perm / (merkle_ms * 1e-3) / 1e9
+        calib = ctx.calibrate_poseidon2()
+        valu_achieved = trace_perms / (merkle_ms * 1e-3) / 1e6
         out = {
             "metric": METRIC,
             "value": value,
@@ -163,9 +162,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": lde_traffic(args.log_n, w),
                          "algorithmic_bytes": lde_bytes, "ms": lde_ms},
             "roofline_valu": {"bound": "valu", "kernel": "trace Merkle tree (Poseidon2 leaf hash + levels)",
-                              "achieved": valu_achieved, "unit": "G Fr-mul/s",
-                              "peak": calib, "frac": (valu_achieved / calib) if calib else None,
-                              "perms": trace_perms, "mul_per_perm": mul_per_perm, "ms": merkle_ms},
+                              "achieved": valu_achieved, "unit": "M perm/s",
+                              "peak": calib, "frac": valu_achieved / calib,
+                              "peak_source": "lsp_calibrate_poseidon2: register-resident chained permutations",
+                              "perms": trace_perms, "fr_mul_per_perm": 230, "ms": merkle_ms},
         }
         if world == 1 and not args.no_cpu_baseline and args.air == "perm":
             out["cpu_baseline"] = cpu_baseline(args)

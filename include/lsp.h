@@ -234,6 +234,10 @@ int lsp_last_timings(const lsp_ctx *ctx, double *ms, const char **names, size_t 
  * independent chains): the calibrated VALU peak the Merkle/Poseidon2
  * roofline is quoted against. */
 int lsp_calibrate_fr_mul(lsp_ctx *ctx, double *gmul_per_s);
+/* Poseidon2-w3 permutation throughput (register-resident chained states,
+ * the device permutation kernels' code): the peak the Merkle kernels'
+ * roofline (bench.py roofline_valu) is quoted against, in M perm/s. */
+int lsp_calibrate_poseidon2(lsp_ctx *ctx, double *mperm_per_s);
 
 /* ------------------------------------------------------------- witness */
 /* Synthetic permutation trace with the witness columns of

@@ -1,6 +1,7 @@
 // extern "C" entry points of liblsp_hip.so (declared in include/lsp.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <thread>
@@ -779,6 +780,35 @@ int lsp_calibrate_fr_mul(lsp_ctx* ctx, double* gmul_per_s) {
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
         *gmul_per_s = (double)nth * iters * 4 / (ms * 1e-3) / 1e9;
+    });
+}
+
+int lsp_calibrate_poseidon2(lsp_ctx* ctx, double* mperm_per_s) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(mperm_per_s, LSP_E_ARG, "null");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        // the peak: best of several grid sizes (2..32 blocks of 256 lanes per CU)
+        const uint32_t iters = 4;
+        Fr* out = ctx->fbuf("calib", (size_t)256 * 256 * 32);
+        LSP_HIP(launch_calib_perm(out, (size_t)256 * 256 * 4, 1, ctx->rc29_dev, ctx->p2.L, ctx->stream));  // warm
+        hipEvent_t e0, e1;
+        LSP_HIP(hipEventCreate(&e0));
+        LSP_HIP(hipEventCreate(&e1));
+        double best = 0;
+        for (size_t per_cu : {2, 4, 8, 16, 32}) {
+            const size_t nth = (size_t)256 * 256 * per_cu;
+            LSP_HIP(hipEventRecord(e0, ctx->stream));
+            LSP_HIP(launch_calib_perm(out, nth, iters, ctx->rc29_dev, ctx->p2.L, ctx->stream));
+            LSP_HIP(hipEventRecord(e1, ctx->stream));
+            LSP_HIP(hipEventSynchronize(e1));
+            float ms = 0;
+            LSP_HIP(hipEventElapsedTime(&ms, e0, e1));
+            best = std::max(best, (double)nth * iters / (ms * 1e-3) / 1e6);
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        *mperm_per_s = best;
     });
 }
 

@@ -188,11 +188,74 @@ LSP_HD Fr fr_mul_cios(const Fr& a, const Fr& b) {
 #include "fr_mul_gfx950.inc"
 #endif
 
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host product: CIOS on 4 x 64-bit words with 128-bit products (the same
+// Montgomery domain, R = 2^256, so bit-identical to the device product).  It
+// serves the transcript, the verifier and the Merkle tree tops the prover
+// finishes on the host.
+namespace host64 {
+constexpr uint64_t P0 = (uint64_t)LSP_MOD0 | ((uint64_t)LSP_MOD1 << 32);
+constexpr uint64_t P1 = (uint64_t)LSP_MOD2 | ((uint64_t)LSP_MOD3 << 32);
+constexpr uint64_t P2 = (uint64_t)LSP_MOD4 | ((uint64_t)LSP_MOD5 << 32);
+constexpr uint64_t P3 = (uint64_t)LSP_MOD6 | ((uint64_t)LSP_MOD7 << 32);
+constexpr uint64_t inv64() {  // r^-1 mod 2^64 (Newton: each step doubles the correct bits)
+    uint64_t x = 1;
+    for (int i = 0; i < 7; ++i) x *= 2 - P0 * x;
+    return x;
+}
+constexpr uint64_t NP = 0 - inv64();  // -r^-1 mod 2^64
+}  // namespace host64
+
+inline Fr fr_mul_host64(const Fr& a, const Fr& b) {
+    using namespace host64;
+    typedef unsigned __int128 u128;
+    static const uint64_t P[4] = {P0, P1, P2, P3};
+    uint64_t x[4], y[4];
+    __builtin_memcpy(x, a.v, 32);
+    __builtin_memcpy(y, b.v, 32);
+    uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+    for (int i = 0; i < 4; ++i) {
+        u128 c = (u128)x[0] * y[i] + t0;
+        t0 = (uint64_t)c;
+        c = (u128)x[1] * y[i] + t1 + (uint64_t)(c >> 64);
+        t1 = (uint64_t)c;
+        c = (u128)x[2] * y[i] + t2 + (uint64_t)(c >> 64);
+        t2 = (uint64_t)c;
+        c = (u128)x[3] * y[i] + t3 + (uint64_t)(c >> 64);
+        t3 = (uint64_t)c;
+        t4 += (uint64_t)(c >> 64);  // t4 stays tiny: inputs < r < 2^253
+        const uint64_t m = t0 * NP;
+        c = (u128)m * P[0] + t0;
+        c = (u128)m * P[1] + t1 + (uint64_t)(c >> 64);
+        t0 = (uint64_t)c;
+        c = (u128)m * P[2] + t2 + (uint64_t)(c >> 64);
+        t1 = (uint64_t)c;
+        c = (u128)m * P[3] + t3 + (uint64_t)(c >> 64);
+        t2 = (uint64_t)c;
+        c = (u128)t4 + (uint64_t)(c >> 64);
+        t3 = (uint64_t)c;
+        t4 = (uint64_t)(c >> 64);
+    }
+    uint64_t r[4] = {t0, t1, t2, t3};
+    // result < 2r: subtract r once if r[] >= P
+    uint64_t d[4];
+    u128 bw = 0;
+    for (int k = 0; k < 4; ++k) {
+        const u128 v = (u128)r[k] - P[k] - (uint64_t)bw;
+        d[k] = (uint64_t)v;
+        bw = (v >> 64) & 1;
+    }
+    Fr out;
+    __builtin_memcpy(out.v, (t4 || !bw) ? d : r, 32);
+    return out;
+}
+#endif
+
 LSP_HD Fr fr_mul(const Fr& a, const Fr& b) {
 #if defined(__HIP_DEVICE_COMPILE__)
     return fr_mul_dev(a, b);
 #else
-    return fr_mul_cios(a, b);
+    return fr_mul_host64(a, b);
 #endif
 }
 

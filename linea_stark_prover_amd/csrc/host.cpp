@@ -3,6 +3,7 @@
 #include "host.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 namespace lsp {
@@ -52,6 +53,57 @@ uint32_t log2_exact(size_t n) {
     while (((size_t)1 << b) < n) ++b;
     if (n == 0 || ((size_t)1 << b) != n) throw LspError(LSP_E_SIZE, "height must be a power of two");
     return b;
+}
+
+HostPool::HostPool(unsigned workers) {
+    for (unsigned i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
+}
+
+HostPool::~HostPool() {
+    {
+        std::lock_guard<std::mutex> lk(m_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+}
+
+void HostPool::loop() {
+    uint64_t seen = 0;
+    for (;;) {
+        const std::function<void(size_t)>* job;
+        size_t n;
+        {
+            std::unique_lock<std::mutex> lk(m_);
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            job = job_;
+            n = n_;
+        }
+        for (size_t i; (i = next_.fetch_add(1)) < n;) (*job)(i);
+        std::lock_guard<std::mutex> lk(m_);
+        if (--busy_ == 0) done_.notify_all();
+    }
+}
+
+void HostPool::parallel_for(size_t n, const std::function<void(size_t)>& f) {
+    if (th_.empty() || n < 4) {
+        for (size_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    {
+        std::lock_guard<std::mutex> lk(m_);
+        job_ = &f;
+        n_ = n;
+        next_.store(0);
+        busy_ = (unsigned)th_.size();
+        ++gen_;
+    }
+    cv_.notify_all();
+    for (size_t i; (i = next_.fetch_add(1)) < n;) f(i);
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return busy_ == 0; });
 }
 
 Fr P2Host::hash(const Fr* in, size_t n) const {
@@ -217,6 +269,15 @@ void* lsp_ctx::buf(const std::string& name, size_t bytes) {
         }
     }
     return b.p;
+}
+
+lsp::HostPool& lsp_ctx::host_pool() {
+    if (!pool_) {
+        unsigned n = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+        if (const char* e = std::getenv("LSP_HOST_THREADS")) n = (unsigned)std::max(1L, std::strtol(e, nullptr, 10));
+        pool_.reset(new lsp::HostPool(n - 1));
+    }
+    return *pool_;
 }
 
 const lsp::Fr* lsp_ctx::twiddle(uint32_t logH, bool inverse) {

@@ -3,8 +3,13 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <map>
+#include <memory>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -151,11 +156,36 @@ struct lsp_tree {
 
 namespace lsp {
 struct Comm;
-}
+
+// Small persistent host thread pool: parallel_for over [0, n) with the
+// calling thread participating.  Used for the Merkle tree tops the prover
+// finishes on the host (a few dozen permutations per level).
+class HostPool {
+  public:
+    explicit HostPool(unsigned workers);
+    ~HostPool();
+    void parallel_for(size_t n, const std::function<void(size_t)>& f);
+    unsigned size() const { return (unsigned)th_.size() + 1; }
+
+  private:
+    void loop();
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(size_t)>* job_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    unsigned busy_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+}  // namespace lsp
 
 struct lsp_ctx {
     int device = 0;
     lsp::Comm* comm = nullptr;  // attached communicator of a process-per-GPU sharded prove (owned)
+    std::unique_ptr<lsp::HostPool> pool_;  // lazily created (host_pool())
+    size_t host_tree_top = 128;             // Merkle levels at or below this many digests run on the host
     hipStream_t stream = nullptr;
     lsp::P2Host p2;
     lsp::Fr* rc_dev = nullptr;    // round constants, ark form
@@ -175,5 +205,6 @@ struct lsp_ctx {
     void* buf(const std::string& name, size_t bytes);
     lsp::Fr* fbuf(const std::string& name, size_t n) { return (lsp::Fr*)buf(name, n * sizeof(lsp::Fr)); }
     const lsp::Fr* twiddle(uint32_t logH, bool inverse);
+    lsp::HostPool& host_pool();
     void sync();
 };

@@ -118,6 +118,17 @@ __global__ __launch_bounds__(256) void k_grind(Fr pre0, Fr pre1, Fr pre2, uint32
     }
 }
 
+// Permutation-throughput probe (the peak the Merkle kernels are quoted
+// against): `iters` chained permutations per lane on register-resident states.
+template <uint32_t D>
+__global__ __launch_bounds__(256) void k_calib_perm(Fr* __restrict__ out, uint32_t iters, const F29* __restrict__ rc,
+                                                    uint32_t rf, uint32_t rp) {
+    const size_t t = gtid();
+    F29 s0 = f29_from_fr(fr_from_u64(t + 1)), s1 = f29_from_fr(fr_from_u64(3 * t + 7)), s2 = f29_zero();
+    for (uint32_t i = 0; i < iters; ++i) permute3_f29<D>(s0, s1, s2, rc, rf, rp);
+    out[t] = f29_to_fr(s0);
+}
+
 __global__ void k_rc_to_f29(const Fr* __restrict__ rc, F29* __restrict__ rc29, uint32_t n) {
     const uint32_t i = (uint32_t)gtid();
     if (i < n) rc29[i] = f29_from_fr(rc[i]);
@@ -189,6 +200,12 @@ hipError_t launch_hash_rows(const MatList& m, size_t nrows, Fr* out, const F29* 
     return hipGetLastError();
 }
 
+hipError_t launch_calib_perm(Fr* out, size_t nthreads, uint32_t iters, const F29* rc, P2Layout L, hipStream_t st) {
+    LSP_DISPATCH_D(L, k_calib_perm, dim3(nblocks(nthreads, 256)), dim3(256), 0, st, out, iters, rc, L.rounds_f,
+                   L.rounds_p);
+    return hipGetLastError();
+}
+
 hipError_t launch_grind(const Fr pre[3], uint32_t wlane, uint64_t base, uint64_t count, uint32_t bits,
                         const F29* rc, P2Layout L, unsigned long long* best, hipStream_t st) {
     const unsigned blocks = 256 * 16;
@@ -205,6 +222,20 @@ hipError_t launch_merkle_level(const Fr* src, Fr* dst, size_t nout, const F29* r
     LSP_DISPATCH_DC(L, coop, k_merkle_level, dim3(blocks), dim3(bs), 0, st, src, dst, nout, rc, L.rounds_f,
                     L.rounds_p);
     return hipGetLastError();
+}
+
+hipError_t launch_merkle_levels(Fr* layers, size_t nleaves, size_t stop_len, const F29* rc, P2Layout L,
+                                size_t* off_out, size_t* len_out, hipStream_t st) {
+    size_t off = 0, len = nleaves;
+    while (len > stop_len && len > 1) {
+        hipError_t e = launch_merkle_level(layers + off, layers + off + len, len / 2, rc, L, st);
+        if (e != hipSuccess) return e;
+        off += len;
+        len /= 2;
+    }
+    *off_out = off;
+    *len_out = len;
+    return hipSuccess;
 }
 
 hipError_t launch_merkle_tree(Fr* layers, size_t nleaves, const F29* rc, P2Layout L, hipStream_t st) {

@@ -45,12 +45,18 @@ hipError_t launch_grind(const Fr pre[3], uint32_t wlane, uint64_t base, uint64_t
                         const F29* rc29, P2Layout L, unsigned long long* best, hipStream_t st);
 // full tree above the leaf digests already stored at layers[0..nleaves)
 hipError_t launch_merkle_tree(Fr* layers, size_t nleaves, const F29* rc29, P2Layout L, hipStream_t st);
+// the levels above the leaves while the current layer is longer than stop_len;
+// *off_out / *len_out = offset and length of the last layer written
+hipError_t launch_merkle_levels(Fr* layers, size_t nleaves, size_t stop_len, const F29* rc29, P2Layout L,
+                                size_t* off_out, size_t* len_out, hipStream_t st);
 
 // --------------------------------------------------------- k_field.hip
 // out[i] = 1 / in[i] (Montgomery trick, interleaved chunks); in may alias out? no
 hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st);
 // Fr-mul throughput probe: nthreads lanes x iters x 4 independent products
 hipError_t launch_calib_mul(Fr* out, size_t nthreads, uint32_t iters, hipStream_t st);
+// iters chained Poseidon2 permutations per lane, register-resident (k_hash.hip)
+hipError_t launch_calib_perm(Fr* out, size_t nthreads, uint32_t iters, const F29* rc, P2Layout L, hipStream_t st);
 // out[i] = *ptrs[i]
 hipError_t launch_gather(const uint64_t* ptrs, Fr* out, size_t n, hipStream_t st);
 // Sharded quotient exchange: stage holds 2^logGq blocks of h x cpr values,

@@ -215,6 +215,12 @@ class Context:
         self._chk(L.lib().lsp_calibrate_fr_mul(self.h, ctypes.byref(v)))
         return v.value
 
+    def calibrate_poseidon2(self) -> float:
+        """M Poseidon2 permutations/s (register-resident chained states)."""
+        v = ctypes.c_double()
+        self._chk(L.lib().lsp_calibrate_poseidon2(self.h, ctypes.byref(v)))
+        return v.value
+
     def last_timings(self) -> List[Tuple[str, float]]:
         n = ctypes.c_size_t()
         L.lib().lsp_last_timings(self.h, None, None, 0, ctypes.byref(n))

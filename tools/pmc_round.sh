@@ -10,3 +10,5 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/$
 echo "pmc done"
 timeout -k 10 600 python bench.py --log-n 22 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench22_$TAG.json 2> gpurun_out/bench22_$TAG.err || { tail -20 gpurun_out/bench22_$TAG.err; exit 1; }
 cut -c1-600 gpurun_out/bench22_$TAG.json
+timeout -k 10 900 python bench.py --air wide --log-n 20 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/bench_wide_$TAG.json 2> gpurun_out/bench_wide_$TAG.err || { tail -20 gpurun_out/bench_wide_$TAG.err; exit 1; }
+cut -c1-300 gpurun_out/bench_wide_$TAG.json

@@ -230,6 +230,26 @@ int lsp_verify(const lsp_ctx *ctx, const int32_t *air, size_t air_len, const lsp
  * reference's bench.log */
 int lsp_last_timings(const lsp_ctx *ctx, double *ms, const char **names, size_t cap, size_t *n);
 
+/* Witness generation on the device: the trace crate's
+ * RawPermutationTrace::get_trace (trace/src/permutation.rs:24-93) and
+ * RawLookupTrace::get_trace (trace/src/lookup.rs:46-176).  Raw columns are
+ * column-major (column k at ptr + k*n; lookup B: table t column c at
+ * (t*nbc + c)*n; b_filter: table t at t*n); the block's columns are written
+ * into rows of a row-major trace of width trace_w from column col0 on -- the
+ * layout RawTrace::get_trace assembles (trace/src/lib.rs:94-106), so the
+ * blocks of one trace are generated in push order into one buffer.
+ *   permutation block: a.., b.., b_inverse, check             (na + nb + 2)
+ *   lookup block: a.., b.., a_filter, b_filters.., a_inverses, b_inverses..,
+ *                 multiplicities.., prefix sum                (na + nt(nbc+3) + 3)
+ * LSP_E_STATE if the check column does not end at 1 (permutation) / 0
+ * (lookup), as the reference asserts.  mem applies to every pointer. */
+int lsp_witness_permutation(lsp_ctx *ctx, const lsp_fr *a, uint32_t na, const lsp_fr *b, uint32_t nb, size_t n,
+                            const lsp_fr *alpha, const lsp_fr *delta, lsp_fr *trace, size_t trace_w, size_t col0,
+                            int mem);
+int lsp_witness_lookup(lsp_ctx *ctx, const lsp_fr *a, uint32_t na, const lsp_fr *b, uint32_t ntables, uint32_t nbc,
+                       const lsp_fr *a_filter, const lsp_fr *b_filter, size_t n, const lsp_fr *alpha,
+                       const lsp_fr *delta, lsp_fr *trace, size_t trace_w, size_t col0, int mem);
+
 /* Fr-multiplication throughput of the device multiplier (register-resident
  * independent chains): the calibrated VALU peak the Merkle/Poseidon2
  * roofline is quoted against. */

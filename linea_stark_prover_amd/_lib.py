@@ -115,6 +115,12 @@ _SIGS = {
                                           ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
                                           ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]),
     "lsp_calibrate_fr_mul": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
+    "lsp_witness_permutation": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_uint32, c_fr_p, ctypes.c_uint32,
+                                               ctypes.c_size_t, c_fr_p, c_fr_p, c_fr_p, ctypes.c_size_t,
+                                               ctypes.c_size_t, ctypes.c_int]),
+    "lsp_witness_lookup": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_uint32, c_fr_p, ctypes.c_uint32,
+                                          ctypes.c_uint32, c_fr_p, c_fr_p, ctypes.c_size_t, c_fr_p, c_fr_p, c_fr_p,
+                                          ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]),
     "lsp_calibrate_poseidon2": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "lsp_gen_permutation_trace": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, c_fr_p, c_fr_p,
                                                  ctypes.c_int, c_fr_p]),

@@ -783,6 +783,63 @@ int lsp_calibrate_fr_mul(lsp_ctx* ctx, double* gmul_per_s) {
     });
 }
 
+// ------------------------------------------------- witness generation (F1)
+extern "C++" {
+namespace {
+// the block's rows: straight into a device trace, or via a scratch block and a
+// strided copy into a host trace
+template <class F>
+void witness_block(lsp_ctx* ctx, lsp_fr* trace, size_t n, size_t trace_w, size_t col0, size_t bw, int mem, F&& fill) {
+    LSP_REQUIRE(trace && col0 + bw <= trace_w, LSP_E_ARG, "witness block outside the trace width");
+    if (mem == LSP_MEM_DEVICE) {
+        fill(reinterpret_cast<Fr*>(trace) + col0, trace_w);
+        return;
+    }
+    Fr* blk = ctx->fbuf("wit_block", n * bw);
+    fill(blk, bw);
+    LSP_HIP(hipMemcpy2DAsync(reinterpret_cast<Fr*>(trace) + col0, trace_w * sizeof(Fr), blk, bw * sizeof(Fr),
+                             bw * sizeof(Fr), n, hipMemcpyDeviceToHost, ctx->stream));
+    ctx->sync();
+}
+}  // namespace
+}
+
+int lsp_witness_permutation(lsp_ctx* ctx, const lsp_fr* a, uint32_t na, const lsp_fr* b, uint32_t nb, size_t n,
+                            const lsp_fr* alpha, const lsp_fr* delta, lsp_fr* trace, size_t trace_w, size_t col0,
+                            int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && alpha && delta && na >= 1 && nb >= 1 && n >= 1, LSP_E_ARG, "bad witness arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const Fr* da = dev_in(ctx, a, (size_t)na * n, mem, "wit_a");
+        const Fr* db = dev_in(ctx, b, (size_t)nb * n, mem, "wit_b");
+        const Fr al = to_fr(*alpha), de = to_fr(*delta);
+        witness_block(ctx, trace, n, trace_w, col0, (size_t)na + nb + 2, mem, [&](Fr* out, size_t stride) {
+            witness_permutation_device(ctx, da, na, db, nb, n, al, de, out, stride);
+        });
+    });
+}
+
+int lsp_witness_lookup(lsp_ctx* ctx, const lsp_fr* a, uint32_t na, const lsp_fr* b, uint32_t ntables, uint32_t nbc,
+                       const lsp_fr* a_filter, const lsp_fr* b_filter, size_t n, const lsp_fr* alpha,
+                       const lsp_fr* delta, lsp_fr* trace, size_t trace_w, size_t col0, int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && alpha && delta && na >= 1 && ntables >= 1 && nbc >= 1 && n >= 1, LSP_E_ARG,
+                    "bad witness arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const Fr* da = dev_in(ctx, a, (size_t)na * n, mem, "wit_a");
+        const Fr* db = dev_in(ctx, b, (size_t)ntables * nbc * n, mem, "wit_b");
+        const Fr* daf = dev_in(ctx, a_filter, n, mem, "wit_af");
+        const Fr* dbf = dev_in(ctx, b_filter, (size_t)ntables * n, mem, "wit_bf");
+        const Fr al = to_fr(*alpha), de = to_fr(*delta);
+        const size_t bw = (size_t)na + (size_t)ntables * (nbc + 3) + 3;
+        witness_block(ctx, trace, n, trace_w, col0, bw, mem, [&](Fr* out, size_t stride) {
+            witness_lookup_device(ctx, da, na, db, ntables, nbc, daf, dbf, n, al, de, out, stride);
+        });
+    });
+}
+
 int lsp_calibrate_poseidon2(lsp_ctx* ctx, double* mperm_per_s) {
     return guarded(ctx, [&] {
         LSP_REQUIRE(mperm_per_s, LSP_E_ARG, "null");

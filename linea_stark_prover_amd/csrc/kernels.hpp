@@ -64,6 +64,28 @@ hipError_t launch_gather(const uint64_t* ptrs, Fr* out, size_t n, hipStream_t st
 // h x q chunk matrix (q = cpr << logGq), out[k*q + j].
 hipError_t launch_assemble_chunks(const Fr* stage, uint32_t logGq, size_t cpr, size_t h, Fr* out, hipStream_t st);
 
+// ----------------------------------------------------- k_witness.hip
+// (trace crate semantics; see k_witness.hip)
+size_t witness_scratch_bytes(size_t n, uint32_t ntables);
+// trace row i (stride ostride): a cols, b cols; al/bl = row combination + delta
+hipError_t launch_perm_rows(const Fr* a, uint32_t na, const Fr* b, uint32_t nb, size_t n, Fr alpha, Fr delta,
+                            Fr* out, size_t ostride, Fr* al, Fr* bl, hipStream_t st);
+// trace row i: a cols, b tables, a_filter, b_filters; comb / den: (1 + nt) x n
+hipError_t launch_lookup_rows(const Fr* a, uint32_t na, const Fr* b, uint32_t nt, uint32_t nbc, const Fr* afil,
+                              const Fr* bfil, size_t n, Fr alpha, Fr delta, Fr* out, size_t ostride, Fr* comb,
+                              Fr* den, hipStream_t st);
+hipError_t launch_mul_vec(const Fr* x, const Fr* y, size_t n, Fr* out, hipStream_t st);
+hipError_t launch_put_col(const Fr* v, size_t n, Fr* out, size_t ostride, uint32_t col, hipStream_t st);
+// inclusive prefix product (product = true) or sum over Fr
+hipError_t launch_fr_scan(const Fr* in, Fr* out, size_t n, bool product, void* scratch, size_t scratch_bytes,
+                          hipStream_t st);
+// LogUp multiplicities occ[t][i] (RawLookupTrace::get_trace's occurrence map)
+hipError_t launch_lookup_occurrences(const Fr* comb, size_t n, uint32_t nt, const Fr* afil, const Fr* bfil,
+                                     uint32_t* occ, void* scratch, size_t scratch_bytes, hipStream_t st);
+// a_inverses / b_inverses / multiplicities columns from col_ainv on, and the LogUp terms
+hipError_t launch_lookup_terms(const Fr* inv, const uint32_t* occ, const Fr* afil, size_t n, uint32_t nt, Fr* out,
+                               size_t ostride, uint32_t col_ainv, Fr* term, hipStream_t st);
+
 // ----------------------------------------------------- k_quotient.hip
 struct QuotientArgs {
     const Fr* lde;      // N x w row-major, bit-reversed LDE

@@ -22,6 +22,12 @@ std::vector<uint8_t> serialize(const lsp_proof& p);
 Comm* make_callback_comm(const lsp_comm_ops& ops);
 void rccl_unique_id(uint8_t out[128]);
 Comm* make_rccl_comm(const uint8_t id[128], int rank, int size);
+// witness blocks on the device (witness.cpp): rows written at out + i * ostride
+void witness_permutation_device(lsp_ctx* ctx, const Fr* a, uint32_t na, const Fr* b, uint32_t nb, size_t n,
+                                const Fr& alpha, const Fr& delta, Fr* out, size_t ostride);
+void witness_lookup_device(lsp_ctx* ctx, const Fr* a, uint32_t na, const Fr* b, uint32_t nt, uint32_t nbc,
+                           const Fr* afil, const Fr* bfil, size_t n, const Fr& alpha, const Fr& delta, Fr* out,
+                           size_t ostride);
 // 0 = accept, otherwise the failing check (host CPU verifier)
 int verify_host(const lsp_ctx* ctx, const Air& air, const Fr* pub, size_t npub, const uint8_t* b, size_t n);
 }  // namespace lsp

@@ -6,6 +6,7 @@
 //
 // Layout follows RawTrace: lookup traces first, then permutation traces
 // (trace/src/lib.rs:81-89), each config shifted by the columns already pushed.
+#include <algorithm>
 #include <cstring>
 #include <unordered_map>
 #include <vector>
@@ -252,3 +253,58 @@ extern "C" int lsp_gen_wide_trace(uint64_t seed, uint32_t log_n, uint32_t nlooku
         return LSP_E_STATE;
     }
 }
+
+// ------------------------------------------------- device witness (F1)
+namespace lsp {
+// RawPermutationTrace::get_trace on the device: columns a.., b.., b_inverse,
+// check (prefix product of (a_comb + delta) / (b_comb + delta), must end at 1)
+void witness_permutation_device(lsp_ctx* ctx, const Fr* a, uint32_t na, const Fr* b, uint32_t nb, size_t n,
+                                const Fr& alpha, const Fr& delta, Fr* out, size_t ostride) {
+    hipStream_t st = ctx->stream;
+    Fr* al = ctx->fbuf("wit_al", n);
+    Fr* bl = ctx->fbuf("wit_bl", n);
+    Fr* binv = ctx->fbuf("wit_binv", n);
+    Fr* chk = ctx->fbuf("wit_chk", n);
+    const size_t sb = witness_scratch_bytes(n, 0);
+    void* scratch = ctx->buf("wit_scratch", sb);
+    LSP_HIP(launch_perm_rows(a, na, b, nb, n, alpha, delta, out, ostride, al, bl, st));
+    LSP_HIP(launch_batch_inverse(bl, binv, n, st));
+    LSP_HIP(launch_mul_vec(al, binv, n, al, st));
+    LSP_HIP(launch_fr_scan(al, chk, n, true, scratch, sb, st));
+    LSP_HIP(launch_put_col(binv, n, out, ostride, na + nb, st));
+    LSP_HIP(launch_put_col(chk, n, out, ostride, na + nb + 1, st));
+    Fr last;
+    LSP_HIP(hipMemcpyAsync(&last, chk + n - 1, sizeof(Fr), hipMemcpyDeviceToHost, st));
+    LSP_HIP(hipStreamSynchronize(st));
+    LSP_REQUIRE(fr_eq(last, fr_one()), LSP_E_STATE,
+                "failed to check constrain: check column should be 1 on the last row");
+}
+
+// RawLookupTrace::get_trace on the device: columns a.., b tables.., a_filter,
+// b_filters.., a_inverses, b_inverses.., multiplicities.., prefix sum (must end at 0)
+void witness_lookup_device(lsp_ctx* ctx, const Fr* a, uint32_t na, const Fr* b, uint32_t nt, uint32_t nbc,
+                           const Fr* afil, const Fr* bfil, size_t n, const Fr& alpha, const Fr& delta, Fr* out,
+                           size_t ostride) {
+    hipStream_t st = ctx->stream;
+    const size_t m = n * (1 + (size_t)nt);
+    Fr* comb = ctx->fbuf("wit_comb", m);
+    Fr* den = ctx->fbuf("wit_den", m);
+    Fr* inv = ctx->fbuf("wit_inv", m);
+    uint32_t* occ = (uint32_t*)ctx->buf("wit_occ", std::max<size_t>(1, n * nt) * sizeof(uint32_t));
+    Fr* term = ctx->fbuf("wit_term", n);
+    Fr* psum = ctx->fbuf("wit_psum", n);
+    const size_t sb = witness_scratch_bytes(n, nt);
+    void* scratch = ctx->buf("wit_scratch", sb);
+    LSP_HIP(launch_lookup_rows(a, na, b, nt, nbc, afil, bfil, n, alpha, delta, out, ostride, comb, den, st));
+    LSP_HIP(launch_batch_inverse(den, inv, m, st));
+    LSP_HIP(launch_lookup_occurrences(comb, n, nt, afil, bfil, occ, scratch, sb, st));
+    const uint32_t col_ainv = na + nt * nbc + 1 + nt;
+    LSP_HIP(launch_lookup_terms(inv, occ, afil, n, nt, out, ostride, col_ainv, term, st));
+    LSP_HIP(launch_fr_scan(term, psum, n, false, scratch, sb, st));
+    LSP_HIP(launch_put_col(psum, n, out, ostride, col_ainv + 1 + 2 * nt, st));
+    Fr last;
+    LSP_HIP(hipMemcpyAsync(&last, psum + n - 1, sizeof(Fr), hipMemcpyDeviceToHost, st));
+    LSP_HIP(hipStreamSynchronize(st));
+    LSP_REQUIRE(fr_is_zero(last), LSP_E_STATE, "failed to check constrain: check column should be 0 on the last row");
+}
+}  // namespace lsp

@@ -1,0 +1,183 @@
+"""The reference's ``trace`` crate on the device.
+
+``RawPermutationTrace`` / ``RawLookupTrace`` hold raw columns (trace/src/
+permutation.rs:9-14, trace/src/lookup.rs:10-17) as Montgomery-form Fr arrays
+of shape (n, 4) uint64; ``RawTrace.push_traces`` (trace/src/lib.rs:62-92)
+pads every block to the common height, then generates each block's witness
+columns on the GPU (lsp_witness_lookup / lsp_witness_permutation: row
+combinations, batch inversion, prefix products / sums, LogUp
+multiplicities) directly into one row-major device trace in push order
+(lookups first), returning the shifted AirConfigs.  ``get_trace`` returns the
+device pointer (what ``Context.prove`` takes) or a host copy.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib as L
+from .air import AirLookupConfig, AirPermutationConfig, LineaAIR
+from .field import to_mont
+from .prover import Context, _fr_arr, _ptr
+
+
+def _col(c) -> np.ndarray:
+    return _fr_arr(c).reshape(-1, 4)
+
+
+def _pad(c: np.ndarray, n: int) -> np.ndarray:
+    """Vec::resize(n, [0u8; 32])"""
+    if c.shape[0] == n:
+        return c
+    out = np.zeros((n, 4), np.uint64)
+    out[:c.shape[0]] = c
+    return out
+
+
+@dataclass
+class RawPermutationTrace:
+    a: List[np.ndarray]
+    b: List[np.ndarray]
+    name: str = ""
+
+    def get_max_height(self) -> int:  # trace/src/permutation.rs:120-132
+        return max(len(c) for c in list(self.a) + list(self.b))
+
+    def width(self) -> int:
+        return len(self.a) + len(self.b) + 2
+
+
+@dataclass
+class RawLookupTrace:
+    a: List[np.ndarray]
+    b: List[List[np.ndarray]]
+    a_filter: Optional[np.ndarray] = None
+    b_filter: List[np.ndarray] = field(default_factory=list)
+    name: str = ""
+
+    def fill_filters(self) -> None:
+        """RawLookupTrace::read_file's defaults (trace/src/lookup.rs:25-41): a
+        missing filter entry is 1 (enabled)."""
+        one = to_mont([1])[0]
+        n = len(self.a[0])
+        af = np.zeros((0, 4), np.uint64) if self.a_filter is None else _col(self.a_filter)
+        if len(af) < n:
+            af = np.concatenate([af, np.tile(one, (n - len(af), 1))])
+        self.a_filter = af
+        bfs = [_col(f) for f in self.b_filter]
+        while len(bfs) < len(self.b):
+            bfs.append(np.zeros((0, 4), np.uint64))
+        for t, f in enumerate(bfs):
+            m = len(self.b[t][0])
+            if len(f) < m:
+                bfs[t] = np.concatenate([f, np.tile(one, (m - len(f), 1))])
+        self.b_filter = bfs
+
+    def get_max_height(self) -> int:  # trace/src/lookup.rs:216-229
+        return max([len(c) for c in self.a] + [len(c) for t in self.b for c in t])
+
+    def width(self) -> int:
+        return len(self.a) + len(self.b) * (len(self.b[0]) + 3) + 3
+
+
+class RawTrace:
+    """trace/src/lib.rs:17-107: the blocks of one trace, generated on `ctx`'s GPU."""
+
+    def __init__(self, ctx: Context, challenges: Sequence[np.ndarray]):
+        assert len(challenges) == 2, "Two challenges should be provided"
+        self.ctx = ctx
+        self.alpha = _col(challenges[0])[0].copy()
+        self.delta = _col(challenges[1])[0].copy()
+        self.height = 0
+        self.width = 0
+        self.ptr: Optional[int] = None
+
+    def push_traces(self, permutation_traces: Sequence[RawPermutationTrace],
+                    lookup_traces: Sequence[RawLookupTrace]) -> List:
+        h = 0
+        for t in list(lookup_traces) + list(permutation_traces):
+            h = max(h, t.get_max_height())
+        self.height = h
+        self.width = sum(t.width() for t in lookup_traces) + sum(t.width() for t in permutation_traces)
+        if self.ptr is not None:
+            self.ctx.dev_free(self.ptr)
+        self.ptr = self.ctx.dev_alloc(h * self.width * 32)
+        cfgs, col = [], 0
+        for lt in lookup_traces:  # lookups first (trace/src/lib.rs:81-89)
+            cfg = self._push_lookup(lt, col)
+            cfgs.append(cfg)
+            col += lt.width()
+        for pt in permutation_traces:
+            cfgs.append(self._push_permutation(pt, col))
+            col += pt.width()
+        return cfgs
+
+    def air(self, cfgs) -> LineaAIR:
+        return LineaAIR(list(cfgs))
+
+    def _push_permutation(self, pt: RawPermutationTrace, col0: int) -> AirPermutationConfig:
+        n = self.height
+        a = np.ascontiguousarray(np.stack([_pad(_col(c), n) for c in pt.a]))
+        b = np.ascontiguousarray(np.stack([_pad(_col(c), n) for c in pt.b]))
+        na, nb = a.shape[0], b.shape[0]
+        da = self._upload(a)
+        db = self._upload(b)
+        try:
+            self.ctx._chk(L.lib().lsp_witness_permutation(
+                self.ctx.h, da, na, db, nb, n, _ptr(self.alpha), _ptr(self.delta), self.ptr, self.width, col0,
+                L.LSP_MEM_DEVICE))
+        finally:
+            self.ctx.dev_free(da)
+            self.ctx.dev_free(db)
+        cfg = AirPermutationConfig(list(range(na)), list(range(na, na + nb)), na + nb, na + nb + 1)
+        cfg.shift(col0)
+        return cfg
+
+    def _push_lookup(self, lt: RawLookupTrace, col0: int) -> AirLookupConfig:
+        n = self.height
+        lt.fill_filters()
+        nt, nbc, na = len(lt.b), len(lt.b[0]), len(lt.a)
+        a = np.ascontiguousarray(np.stack([_pad(_col(c), n) for c in lt.a]))
+        b = np.ascontiguousarray(np.stack([_pad(_col(c), n) for t in lt.b for c in t]))
+        af = np.ascontiguousarray(_pad(lt.a_filter, n))
+        bf = np.ascontiguousarray(np.stack([_pad(f, n) for f in lt.b_filter]))
+        ptrs = [self._upload(x) for x in (a, b, af, bf)]
+        try:
+            self.ctx._chk(L.lib().lsp_witness_lookup(
+                self.ctx.h, ptrs[0], na, ptrs[1], nt, nbc, ptrs[2], ptrs[3], n, _ptr(self.alpha),
+                _ptr(self.delta), self.ptr, self.width, col0, L.LSP_MEM_DEVICE))
+        finally:
+            for p in ptrs:
+                self.ctx.dev_free(p)
+        # column ids (trace/src/lookup.rs:178-214)
+        a_ids = list(range(na))
+        b_ids = [[na + t * nbc + c for c in range(nbc)] for t in range(nt)]
+        af_id = na + nt * nbc
+        bf_ids = [af_id + 1 + t for t in range(nt)]
+        ai_id = af_id + 1 + nt
+        bi_ids = [ai_id + 1 + t for t in range(nt)]
+        oc_ids = [ai_id + 1 + nt + t for t in range(nt)]
+        cfg = AirLookupConfig(a_ids, b_ids, af_id, bf_ids, ai_id, bi_ids, oc_ids, ai_id + 1 + 2 * nt)
+        cfg.shift(col0)
+        return cfg
+
+    def _upload(self, x: np.ndarray) -> int:
+        p = self.ctx.dev_alloc(max(x.nbytes, 32))
+        self.ctx.h2d(p, x)
+        return p
+
+    def get_trace(self, host: bool = False):
+        """(device pointer, height, width), or the (height, width, 4) host matrix"""
+        if not host:
+            return self.ptr, self.height, self.width
+        out = np.zeros((self.height, self.width, 4), np.uint64)
+        self.ctx.d2h(out, self.ptr)
+        return out
+
+    def close(self):
+        if self.ptr is not None:
+            self.ctx.dev_free(self.ptr)
+            self.ptr = None

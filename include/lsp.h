@@ -250,6 +250,26 @@ int lsp_witness_lookup(lsp_ctx *ctx, const lsp_fr *a, uint32_t na, const lsp_fr 
                        const lsp_fr *a_filter, const lsp_fr *b_filter, size_t n, const lsp_fr *alpha,
                        const lsp_fr *delta, lsp_fr *trace, size_t trace_w, size_t col0, int mem);
 
+/* Trace input: one CBOR RawPermutationTrace
+ * (trace/src/permutation.rs:9-22) or RawLookupTrace (trace/src/lookup.rs:
+ * 10-44) as serde/ciborium write them ([u8; 32] words big-endian, reduced
+ * with from_be_bytes_mod_order; missing lookup filter entries = 1, as
+ * read_file pads them).  kind = LSP_AIR_PERMUTATION / LSP_AIR_LOOKUP;
+ * permutation: ntables = number of b columns, nbc = 0.
+ * lsp_raw_trace_push = RawTrace::push_permutation / push_lookup
+ * (trace/src/lib.rs:38-60): resize to `height` (zero words) and generate the
+ * block's witness on the GPU into trace columns col0 .. col0 + width - 1. */
+typedef struct lsp_raw_trace lsp_raw_trace;
+int lsp_raw_trace_parse(const uint8_t *cbor, size_t len, lsp_raw_trace **out);
+int lsp_raw_trace_shape(const lsp_raw_trace *t, int *kind, uint32_t *na, uint32_t *ntables, uint32_t *nbc,
+                        size_t *max_height, size_t *width);
+/* raw columns resized to `height`, column-major (a.., b.. table-major,
+ * lookup: a_filter, b_filters..); out == NULL -> *n = element count */
+int lsp_raw_trace_columns(const lsp_raw_trace *t, size_t height, lsp_fr *out, size_t cap, size_t *n);
+int lsp_raw_trace_push(lsp_ctx *ctx, const lsp_raw_trace *t, size_t height, const lsp_fr *alpha, const lsp_fr *delta,
+                       lsp_fr *trace, size_t trace_w, size_t col0, int mem);
+int lsp_raw_trace_free(lsp_raw_trace *t);
+
 /* Fr-multiplication throughput of the device multiplier (register-resident
  * independent chains): the calibrated VALU peak the Merkle/Poseidon2
  * roofline is quoted against. */

@@ -121,6 +121,16 @@ _SIGS = {
     "lsp_witness_lookup": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_uint32, c_fr_p, ctypes.c_uint32,
                                           ctypes.c_uint32, c_fr_p, c_fr_p, ctypes.c_size_t, c_fr_p, c_fr_p, c_fr_p,
                                           ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]),
+    "lsp_raw_trace_parse": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    "lsp_raw_trace_shape": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                           ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                           ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_size_t),
+                                           ctypes.POINTER(ctypes.c_size_t)]),
+    "lsp_raw_trace_columns": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, c_fr_p, ctypes.c_size_t,
+                                             ctypes.POINTER(ctypes.c_size_t)]),
+    "lsp_raw_trace_push": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, c_fr_p, c_fr_p, c_fr_p,
+                                          ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]),
+    "lsp_raw_trace_free": (ctypes.c_int, [ctypes.c_void_p]),
     "lsp_calibrate_poseidon2": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "lsp_gen_permutation_trace": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, c_fr_p, c_fr_p,
                                                  ctypes.c_int, c_fr_p]),

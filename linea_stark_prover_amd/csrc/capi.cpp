@@ -840,6 +840,76 @@ int lsp_witness_lookup(lsp_ctx* ctx, const lsp_fr* a, uint32_t na, const lsp_fr*
     });
 }
 
+// ------------------------------------------------------ trace input (F4)
+int lsp_raw_trace_parse(const uint8_t* cbor, size_t len, lsp_raw_trace** out) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(cbor && out, LSP_E_ARG, "null input");
+        *out = parse_raw_trace(cbor, len);
+    });
+}
+
+int lsp_raw_trace_shape(const lsp_raw_trace* t, int* kind, uint32_t* na, uint32_t* ntables, uint32_t* nbc,
+                        size_t* max_height, size_t* width) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(t, LSP_E_ARG, "null trace");
+        size_t h, w;
+        raw_trace_shape(*t, h, w);
+        if (kind) *kind = t->kind;
+        if (na) *na = (uint32_t)t->a.size();
+        if (ntables) *ntables = t->ntables;
+        if (nbc) *nbc = t->nbc;
+        if (max_height) *max_height = h;
+        if (width) *width = w;
+    });
+}
+
+int lsp_raw_trace_columns(const lsp_raw_trace* t, size_t height, lsp_fr* out, size_t cap, size_t* n) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(t && n, LSP_E_ARG, "null argument");
+        const std::vector<Fr> cols = raw_trace_columns(*t, height);
+        *n = cols.size();
+        if (out) {
+            LSP_REQUIRE(cap >= cols.size(), LSP_E_ARG, "buffer too small");
+            std::memcpy(out, cols.data(), cols.size() * sizeof(Fr));
+        }
+    });
+}
+
+int lsp_raw_trace_push(lsp_ctx* ctx, const lsp_raw_trace* t, size_t height, const lsp_fr* alpha, const lsp_fr* delta,
+                       lsp_fr* trace, size_t trace_w, size_t col0, int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && t && alpha && delta && height >= 1, LSP_E_ARG, "bad raw trace push arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const std::vector<Fr> cols = raw_trace_columns(*t, height);  // RawTrace resize: zero words
+        Fr* d = ctx->fbuf("raw_cols", cols.size());
+        LSP_HIP(hipMemcpyAsync(d, cols.data(), cols.size() * sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+        const Fr al = to_fr(*alpha), de = to_fr(*delta);
+        const uint32_t na = (uint32_t)t->a.size();
+        size_t h, w;
+        raw_trace_shape(*t, h, w);
+        if (t->kind == LSP_AIR_PERMUTATION) {
+            const uint32_t nb = (uint32_t)t->b.size();
+            witness_block(ctx, trace, height, trace_w, col0, w, mem, [&](Fr* out, size_t stride) {
+                witness_permutation_device(ctx, d, na, d + (size_t)na * height, nb, height, al, de, out, stride);
+            });
+        } else {
+            const Fr* b = d + (size_t)na * height;
+            const Fr* af = b + (size_t)t->ntables * t->nbc * height;
+            const Fr* bf = af + height;
+            witness_block(ctx, trace, height, trace_w, col0, w, mem, [&](Fr* out, size_t stride) {
+                witness_lookup_device(ctx, d, na, b, t->ntables, t->nbc, af, bf, height, al, de, out, stride);
+            });
+        }
+        ctx->sync();  // `cols` must outlive the upload
+    });
+}
+
+int lsp_raw_trace_free(lsp_raw_trace* t) {
+    delete t;
+    return LSP_OK;
+}
+
 int lsp_calibrate_poseidon2(lsp_ctx* ctx, double* mperm_per_s) {
     return guarded(ctx, [&] {
         LSP_REQUIRE(mperm_per_s, LSP_E_ARG, "null");

@@ -146,6 +146,16 @@ struct lsp_proof {
     std::vector<lsp::lsp_query> queries;
 };
 
+// a parsed CBOR RawPermutationTrace / RawLookupTrace (cbor.cpp)
+struct lsp_raw_trace {
+    int kind = 0;  // LSP_AIR_PERMUTATION or LSP_AIR_LOOKUP
+    std::string name;
+    std::vector<std::vector<lsp::Fr>> a, b;  // lookup: b = the tables' columns, table-major
+    uint32_t ntables = 0, nbc = 0;           // permutation: ntables = number of b columns
+    std::vector<lsp::Fr> a_filter;
+    std::vector<std::vector<lsp::Fr>> b_filter;
+};
+
 struct lsp_tree {
     lsp_ctx* ctx = nullptr;
     size_t height = 0;

@@ -28,6 +28,10 @@ void witness_permutation_device(lsp_ctx* ctx, const Fr* a, uint32_t na, const Fr
 void witness_lookup_device(lsp_ctx* ctx, const Fr* a, uint32_t na, const Fr* b, uint32_t nt, uint32_t nbc,
                            const Fr* afil, const Fr* bfil, size_t n, const Fr& alpha, const Fr& delta, Fr* out,
                            size_t ostride);
+// CBOR RawPermutationTrace / RawLookupTrace (cbor.cpp)
+lsp_raw_trace* parse_raw_trace(const uint8_t* buf, size_t len);
+void raw_trace_shape(const lsp_raw_trace& t, size_t& height, size_t& width);
+std::vector<Fr> raw_trace_columns(const lsp_raw_trace& t, size_t height);
 // 0 = accept, otherwise the failing check (host CPU verifier)
 int verify_host(const lsp_ctx* ctx, const Air& air, const Fr* pub, size_t npub, const uint8_t* b, size_t n);
 }  // namespace lsp

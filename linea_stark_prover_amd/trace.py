@@ -24,6 +24,32 @@ from .field import to_mont
 from .prover import Context, _fr_arr, _ptr
 
 
+def _parse_cbor(data: bytes):
+    """lsp_raw_trace_parse -> (kind, na, ntables, nbc, height, columns (k, height, 4))"""
+    h = ctypes.c_void_p()
+    L.check(L.lib().lsp_raw_trace_parse(data, len(data), ctypes.byref(h)))
+    try:
+        kind, na, nt, nbc = ctypes.c_int(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        mh, w = ctypes.c_size_t(), ctypes.c_size_t()
+        L.check(L.lib().lsp_raw_trace_shape(h, ctypes.byref(kind), ctypes.byref(na), ctypes.byref(nt),
+                                            ctypes.byref(nbc), ctypes.byref(mh), ctypes.byref(w)))
+        n = ctypes.c_size_t()
+        L.check(L.lib().lsp_raw_trace_columns(h, mh.value, None, 0, ctypes.byref(n)))
+        cols = np.zeros((n.value, 4), np.uint64)
+        L.check(L.lib().lsp_raw_trace_columns(h, mh.value, _ptr(cols), n.value, ctypes.byref(n)))
+        height = mh.value
+        return kind.value, na.value, nt.value, nbc.value, height, cols.reshape(-1, height, 4) if height else cols
+    finally:
+        L.lib().lsp_raw_trace_free(h)
+
+
+def _read(path_or_bytes) -> bytes:
+    if isinstance(path_or_bytes, (bytes, bytearray)):
+        return bytes(path_or_bytes)
+    with open(path_or_bytes, "rb") as f:
+        return f.read()
+
+
 def _col(c) -> np.ndarray:
     return _fr_arr(c).reshape(-1, 4)
 
@@ -43,6 +69,14 @@ class RawPermutationTrace:
     b: List[np.ndarray]
     name: str = ""
 
+    @staticmethod
+    def read_file(path_or_bytes) -> "RawPermutationTrace":
+        """trace/src/permutation.rs:17-22 (CBOR via the library's parser)"""
+        kind, na, nb, _, h, cols = _parse_cbor(_read(path_or_bytes))
+        if kind != L.LSP_AIR_PERMUTATION:
+            raise ValueError("not a RawPermutationTrace")
+        return RawPermutationTrace([cols[k] for k in range(na)], [cols[na + k] for k in range(nb)])
+
     def get_max_height(self) -> int:  # trace/src/permutation.rs:120-132
         return max(len(c) for c in list(self.a) + list(self.b))
 
@@ -57,6 +91,18 @@ class RawLookupTrace:
     a_filter: Optional[np.ndarray] = None
     b_filter: List[np.ndarray] = field(default_factory=list)
     name: str = ""
+
+    @staticmethod
+    def read_file(path_or_bytes) -> "RawLookupTrace":
+        """trace/src/lookup.rs:20-44 (CBOR via the library's parser; filter defaults applied)"""
+        kind, na, nt, nbc, h, cols = _parse_cbor(_read(path_or_bytes))
+        if kind != L.LSP_AIR_LOOKUP:
+            raise ValueError("not a RawLookupTrace")
+        a = [cols[k] for k in range(na)]
+        b = [[cols[na + t * nbc + c] for c in range(nbc)] for t in range(nt)]
+        af = cols[na + nt * nbc]
+        bf = [cols[na + nt * nbc + 1 + t] for t in range(nt)]
+        return RawLookupTrace(a, b, af, bf)
 
     def fill_filters(self) -> None:
         """RawLookupTrace::read_file's defaults (trace/src/lookup.rs:25-41): a

@@ -177,3 +177,44 @@ def test_large_lookup_self_consistent(gpu_ctx):
     pub = np.concatenate([to_mont([al]), to_mont([de])])
     assert gpu_ctx.verify(gpu_ctx.prove(ptr, air, pub, h, w), air, pub)
     rt.close()
+
+
+def test_cbor_inputs_to_proof(gpu_ctx):
+    """F4 -> F1 -> prove: CBOR traces parsed natively, witness generated on the
+    GPU, equal to the oracle's witness; lsp_raw_trace_push gives the same block"""
+    import ctypes
+    import os
+    import sys
+    from linea_stark_prover_amd import _lib as L
+    from linea_stark_prover_amd.field import to_mont
+    from linea_stark_prover_amd.prover import _ptr
+    from linea_stark_prover_amd.trace import RawLookupTrace, RawPermutationTrace, RawTrace
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import cbor_enc as C
+    al, de = _challenges()
+    n = 128
+    a, b, af, bf = _lookup_case(n, 2, 2, 31)
+    pa, pb = _perm_case(n, 2, 32)
+    lbytes = C.enc(C.lookup_trace(a, b, af, bf))
+    pbytes = C.enc(C.permutation_trace(pa, pb), words_as_bytes=True)
+    _, lcols = O.lookup_witness(a, b, af, bf, al, de)
+    _, pcols = O.perm_witness(pa, pb, al, de)
+    exp = np.stack(_mont_cols(lcols + pcols), axis=1)
+    rt = RawTrace(gpu_ctx, [to_mont([al]), to_mont([de])])
+    cfgs = rt.push_traces([RawPermutationTrace.read_file(pbytes)], [RawLookupTrace.read_file(lbytes)])
+    assert np.array_equal(rt.get_trace(host=True), exp)
+    # the C-ABI path: parse + push the lookup block into a host trace
+    h = ctypes.c_void_p()
+    L.check(L.lib().lsp_raw_trace_parse(lbytes, len(lbytes), ctypes.byref(h)))
+    host = np.zeros((n, exp.shape[1], 4), np.uint64)
+    alm, dem = to_mont([al]), to_mont([de])
+    gpu_ctx._chk(L.lib().lsp_raw_trace_push(gpu_ctx.h, h, n, _ptr(alm), _ptr(dem), _ptr(host), exp.shape[1], 0,
+                                            L.LSP_MEM_HOST))
+    L.lib().lsp_raw_trace_free(h)
+    lw = len(lcols)
+    assert np.array_equal(host[:, :lw], exp[:, :lw])
+    air = rt.air(cfgs)
+    pub = np.concatenate([alm, dem])
+    ptr, hh, w = rt.get_trace()
+    assert gpu_ctx.verify(gpu_ctx.prove(ptr, air, pub, hh, w), air, pub)
+    rt.close()

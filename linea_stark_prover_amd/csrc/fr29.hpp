@@ -38,10 +38,16 @@ __device__ __forceinline__ constexpr uint32_t p29(int i) {
                   : 0x12ab65u;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(LSP_F29_NO_ASM)
+// the same product / square with one asm block per column (tools/gen_fr29mul.py)
+#include "fr29_mul_gfx950.inc"
+#define LSP_F29_USE_ASM 1
+#endif
+
 // Montgomery product a * b * 2^-261 mod r (lazy: output < 3.3 r for inputs
 // < 32 r).  FIPS, one 64-bit accumulator; -r^-1 mod 2^29 = 2^29 - 1, so the
 // quotient digit is m = -t mod 2^29, and m * r[0] = m clears the low digit.
-__device__ __forceinline__ F29 f29_mul(const F29& a, const F29& b) {
+__device__ __forceinline__ F29 f29_mul_c(const F29& a, const F29& b) {
     uint32_t m[9];
     F29 o;
     uint64_t acc = 0;
@@ -73,7 +79,7 @@ __device__ __forceinline__ F29 f29_mul(const F29& a, const F29& b) {
 // Montgomery square: cross products a_i a_j (i < j) taken once against the
 // doubled limb 2 a_i (< 2^30, products < 2^59): 45 + 72 products instead of
 // 81 + 72.  Column bound: <= 5 such products + 8 m*r products + carry < 2^62.
-__device__ __forceinline__ F29 f29_sqr(const F29& a) {
+__device__ __forceinline__ F29 f29_sqr_c(const F29& a) {
     uint32_t m[9], d[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) d[i] = a.l[i] << 1;
@@ -96,6 +102,22 @@ __device__ __forceinline__ F29 f29_sqr(const F29& a) {
     }
     o.l[8] = (uint32_t)acc;
     return o;
+}
+
+__device__ __forceinline__ F29 f29_mul(const F29& a, const F29& b) {
+#ifdef LSP_F29_USE_ASM
+    return f29_mul_asm(a, b);
+#else
+    return f29_mul_c(a, b);
+#endif
+}
+
+__device__ __forceinline__ F29 f29_sqr(const F29& a) {
+#ifdef LSP_F29_USE_ASM
+    return f29_sqr_asm(a);
+#else
+    return f29_sqr_c(a);
+#endif
 }
 
 // limb-wise sum + carry propagation (no modular reduction)

@@ -1,0 +1,24 @@
+"""Check the bench's event-timed coset_lde_batch (roofline.ms) against the
+rocprofv3 kernel trace of the same LDE (tools/pmc_round.sh 'kt' pass over
+tools/lde_probe.py, 3 calls): per-call sum of the LDE kernels.
+
+    python tools/lde_agreement.py profiles/r01g_lde_kernel_stats.csv profiles/r01g_bench.json [calls]
+"""
+import csv, json, sys
+
+stats, bench = sys.argv[1], sys.argv[2]
+calls = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+rows = list(csv.DictReader(open(stats)))
+lines, tot = [], 0.0
+for r in rows:
+    name = r["Name"].replace("lsp::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
+    if "k_ntt_rm" in name or "k_pow_tables" in name:
+        ms = float(r["TotalDurationNs"]) / calls / 1e6
+        tot += ms
+        lines.append(f"  {name:28s} calls {int(r['Calls']):3d}  avg {float(r['AverageNs']) / 1e3:9.1f} us  per LDE call {ms:7.3f} ms")
+b = json.load(open(bench))["roofline"]
+print("coset_lde_batch (trace, 2^19 x 8 -> 2^22 x 8): rocprofv3 kernel time vs the bench's HIP-event phase")
+print("\n".join(lines))
+print(f"  sum per call (rocprofv3)       {tot:.3f} ms   (k_pow_tables also counts the one-off twiddle tables)")
+print(f"  bench roofline.ms (HIP events)  {b['ms']:.3f} ms   achieved {b['achieved']:.1f} GB/s of {b['peak']:.0f}")
+print(f"  ratio                           {b['ms'] / tot:.3f}")

@@ -210,6 +210,7 @@ struct lsp_ctx {
     };
     std::map<std::string, Buf> pool;
     std::map<std::pair<uint32_t, int>, lsp::Fr*> twiddles;
+    std::map<std::string, const lsp::Fr*> ptabs;  // cached power tables (prove.cpp pow_table), pool-owned
     std::vector<std::pair<std::string, double>> timings;
 
     void* buf(const std::string& name, size_t bytes);

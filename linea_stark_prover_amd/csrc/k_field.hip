@@ -6,16 +6,17 @@
 namespace lsp {
 
 namespace {
-constexpr uint32_t BINV_CHUNK = 32;  // elements per thread: 1 Fermat inverse per 32 elements
-
-// Thread t owns elements t, t+T, t+2T, ... (interleaved so every pass is coalesced)
+// Thread t owns elements t, t+T, t+2T, ... (`chunk` of them, interleaved so every
+// pass is coalesced): a prefix product, one Fermat inverse, the back pass.  The
+// inverse (~380 products) is one instruction stream per wave whatever the
+// chunk, so the launcher sizes the chunk for about one wave per SIMD.
 __global__ __launch_bounds__(256) void k_batch_inverse(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n,
-                                                       size_t T) {
+                                                       size_t T, uint32_t chunk) {
     const size_t t = gtid();
     if (t >= T) return;
     Fr acc = fr_one();
     uint32_t cnt = 0;
-    for (uint32_t j = 0; j < BINV_CHUNK; ++j) {
+    for (uint32_t j = 0; j < chunk; ++j) {
         const size_t i = t + (size_t)j * T;
         if (i >= n) break;
         out[i] = acc;
@@ -65,8 +66,11 @@ __global__ __launch_bounds__(256) void k_assemble_chunks(const Fr* __restrict__ 
 
 hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st) {
     if (!n) return hipSuccess;
-    const size_t T = (n + BINV_CHUNK - 1) / BINV_CHUNK;
-    hipLaunchKernelGGL(k_batch_inverse, dim3(nblocks(T, 256)), dim3(256), 0, st, in, out, n, T);
+    // lanes for one wave per SIMD (256 CUs x 4 SIMDs x 64), 8 .. 256 elements each
+    uint32_t chunk = 8;
+    while (chunk < 256 && (size_t)chunk * 65536 < n) chunk *= 2;
+    const size_t T = (n + chunk - 1) / chunk;
+    hipLaunchKernelGGL(k_batch_inverse, dim3(nblocks(T, 256)), dim3(256), 0, st, in, out, n, T, chunk);
     return hipGetLastError();
 }
 

@@ -48,13 +48,20 @@ __global__ __launch_bounds__(256) void k_interp_partial(const Fr* __restrict__ M
     }
 }
 
+// one workgroup per column: strided partial sums, then a tree in LDS
 __global__ __launch_bounds__(256) void k_sum_partials(const Fr* __restrict__ partial, uint32_t nb, uint32_t w,
                                                       Fr* __restrict__ out) {
-    const size_t c = gtid();
-    if (c >= w) return;
+    __shared__ Fr red[256];
+    const uint32_t c = blockIdx.x;
     Fr acc = fr_zero();
-    for (uint32_t b = 0; b < nb; ++b) acc = fr_add(acc, partial[(size_t)b * w + c]);
-    out[c] = acc;
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) acc = fr_add(acc, partial[(size_t)b * w + c]);
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (uint32_t s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] = fr_add(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[c] = red[0];
 }
 
 __global__ __launch_bounds__(256) void k_reduce_rows(ReduceArgs a) {
@@ -99,7 +106,7 @@ hipError_t launch_interp_partial(const Fr* M, uint32_t w, size_t h, const Fr* in
 }
 
 hipError_t launch_sum_partials(const Fr* partial, uint32_t nb, uint32_t w, Fr* out, hipStream_t st) {
-    hipLaunchKernelGGL(k_sum_partials, dim3(nblocks(w, 256)), dim3(256), 0, st, partial, nb, w, out);
+    hipLaunchKernelGGL(k_sum_partials, dim3(w), dim3(256), 0, st, partial, nb, w, out);
     return hipGetLastError();
 }
 

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -62,13 +63,22 @@ void two_level(uint32_t bits, uint32_t& L1, uint32_t& L2) {
 }
 
 // two-level power table of `base` covering exponents < 2^bits, in pool buffer `name`
+// cached per (base, bits) in the context: the tables of one proof shape (the
+// quotient and LDE domains, every FRI round's w^-1) are the same every proof
 const Fr* pow_table(lsp_ctx* ctx, const std::string& name, const Fr& base, uint32_t bits, uint32_t& L1) {
     uint32_t L2;
     two_level(bits, L1, L2);
-    Fr* tab = ctx->fbuf(name, (1ull << L1) + (1ull << L2));
+    char key[96];
+    std::snprintf(key, sizeof key, "ptab_%u_%08x%08x%08x%08x%08x%08x%08x%08x", bits, base.v[7], base.v[6], base.v[5],
+                  base.v[4], base.v[3], base.v[2], base.v[1], base.v[0]);
+    auto it = ctx->ptabs.find(key);
+    if (it != ctx->ptabs.end()) return it->second;
+    Fr* tab = ctx->fbuf(key, (1ull << L1) + (1ull << L2));
     Fr* b = ctx->fbuf(name + "_base", 1);
     LSP_HIP(hipMemcpyAsync(b, &base, sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
     LSP_HIP(launch_pow_tables(b, 1, L1, L2, nullptr, tab, ctx->stream));
+    LSP_HIP(hipStreamSynchronize(ctx->stream));  // `base` is a host temporary
+    ctx->ptabs[key] = tab;
     return tab;
 }
 

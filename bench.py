@@ -160,11 +160,15 @@ def main():
             "roofline": {"bound": "hbm", "kernel": "coset_lde_batch (trace, w x 2^log_n -> 8x)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": lde_traffic(args.log_n, w),
+                         "valu_issue": valu_issue(["k_ntt_rm"]),
+                         "note": "VALU-bound: valu_issue = share of the chip's VALU issue slots the NTT passes "
+                                 "use (PMC, profiles/*_valu_pmc.json); HBM frac is low by design",
                          "algorithmic_bytes": lde_bytes, "ms": lde_ms},
             "roofline_valu": {"bound": "valu", "kernel": "trace Merkle tree (Poseidon2 leaf hash + levels)",
                               "achieved": valu_achieved, "unit": "M perm/s",
                               "peak": calib, "frac": valu_achieved / calib,
                               "peak_source": "lsp_calibrate_poseidon2: register-resident chained permutations",
+                              "valu_issue": valu_issue(["k_hash_rows1<11u, false>", "k_merkle_level<11u, false>"]),
                               "perms": trace_perms, "fr_mul_per_perm": 230, "ms": merkle_ms},
         }
         if world == 1 and not args.no_cpu_baseline and args.air == "perm":
@@ -173,6 +177,24 @@ def main():
     ctx.dev_free(dtrace)
     ctx.close()
     dist.close()
+
+
+def valu_issue(kernels):
+    """Calls-weighted VALU issue utilisation of the named kernels from the
+    committed PMC passes (tools/pmc_valu.sh -> profiles/*_valu_pmc.json, 2^19
+    prove): SQ_INSTS_VALU * 4 / (1024 SIMDs * cycles); None if absent."""
+    import glob
+    d = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu_pmc.json"))):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+    if not d:
+        return None
+    ks = [v for k, v in d["kernels"].items() if any(k.startswith(p) for p in kernels)]
+    ms = sum(v["ms"] for v in ks)
+    return round(sum(v["valu_issue"] * v["ms"] for v in ks) / ms, 3) if ms else None
 
 
 def lde_traffic(log_n, w):

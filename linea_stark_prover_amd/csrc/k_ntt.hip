@@ -30,53 +30,64 @@ struct NttPass {
     const Fr* twist;    // PASS_FWD_FIRST: two-level tables per (coset[, column])
     uint32_t L1, L2;    // twist table split
     uint32_t twist_per_col;  // 1: table index k*w + c, 0: table index k
-    uint32_t logH, s0, k, logL, logG, CW, w;
+    uint32_t logH, s0, k, logL, logG, w;
+    uint32_t nchunk;    // column chunks of 2^LOGCW per row
     uint64_t narr;      // arrays (cosets) in dst
 };
 
-template <bool DIF, int MODE>
+// One tile: 2^k positions x 2^logG groups x 2^LOGCW columns (power-of-two
+// chunk, so every index below is shifts and masks; rows are 32-bit within
+// an array, H <= 2^31).
+template <bool DIF, int MODE, int LOGCW>
 __global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
     extern __shared__ Fr lds[];
-    const uint32_t K = 1u << p.k, G = 1u << p.logG, CW = p.CW;
+    constexpr uint32_t CW = 1u << LOGCW;
+    const uint32_t K = 1u << p.k, logG = p.logG, G = 1u << logG;
+    const uint32_t logL = p.logL, Lmask = (1u << logL) - 1, rowshift = logL + p.k;
     const uint64_t H = 1ull << p.logH;
-    const uint32_t nchunk = (p.w + CW - 1) / CW;
-    const uint64_t tiles_per_arr = (H >> (p.k + p.logG)) * nchunk;
-    const uint64_t wg = blockIdx.x;
-    const uint64_t arr = wg / tiles_per_arr;
-    const uint64_t rem = wg - arr * tiles_per_arr;
-    const uint64_t tile = rem / nchunk;
-    const uint32_t c0 = (uint32_t)(rem - tile * nchunk) * CW;
+    const uint32_t tiles_per_arr = (uint32_t)(H >> (p.k + logG)) * p.nchunk;
+    const uint32_t wg = blockIdx.x;
+    const uint32_t arr = wg / tiles_per_arr;
+    const uint32_t rem = wg - arr * tiles_per_arr;
+    const uint32_t tile = rem / p.nchunk;
+    const uint32_t c0 = (rem - tile * p.nchunk) << LOGCW;
     const uint32_t cw = min(CW, p.w - c0);
-    const uint64_t Lmask = (1ull << p.logL) - 1;
-    const uint32_t n_el = K * G * CW;
-    const bool t_minor = p.logL < p.logG;
-    Fr* base = p.dst + arr * H * p.w;
-    // ---- load (optionally gathering / twisting)
-    for (uint32_t e = threadIdx.x; e < n_el; e += blockDim.x) {
-        const uint32_t c = e % CW;
-        const uint32_t tg = e / CW;
-        uint32_t t, g;
+    const uint32_t n_el = (K << logG) << LOGCW;
+    const bool t_minor = logL < logG;
+    const uint32_t gid0 = tile << logG;
+    Fr* base = p.dst + (size_t)arr * H * p.w;
+    auto row_of = [&](uint32_t t, uint32_t g) {
+        const uint32_t gid = gid0 + g;
+        return ((gid >> logL) << rowshift) + (t << logL) + (gid & Lmask);
+    };
+    auto split = [&](uint32_t e, uint32_t& t, uint32_t& g, uint32_t& c) {
+        c = e & (CW - 1);
+        const uint32_t tg = e >> LOGCW;
         if (t_minor) {
             t = tg & (K - 1);
             g = tg >> p.k;
         } else {
-            t = tg >> p.logG;
+            t = tg >> logG;
             g = tg & (G - 1);
         }
+    };
+    // ---- load (optionally gathering / twisting)
+    for (uint32_t e = threadIdx.x; e < n_el; e += blockDim.x) {
+        uint32_t t, g, c;
+        split(e, t, g, c);
         if (c >= cw) continue;
-        const uint64_t gid = tile * G + g;
-        const uint64_t row = ((gid >> p.logL) << (p.logL + p.k)) + ((uint64_t)t << p.logL) + (gid & Lmask);
+        const uint32_t row = row_of(t, g);
         Fr v;
         if (MODE == PASS_INV_FIRST) {
-            v = p.src[brev_bits(row, p.logH) * p.w + c0 + c];
+            v = p.src[(size_t)brev_bits(row, p.logH) * p.w + c0 + c];
         } else if (MODE == PASS_FWD_FIRST) {
-            const uint64_t ti = p.twist_per_col ? (arr * p.w + c0 + c) : arr;
+            const size_t ti = p.twist_per_col ? ((size_t)arr * p.w + c0 + c) : arr;
             const Fr* tab = p.twist + ti * ((1ull << p.L1) + (1ull << p.L2));
-            v = fr_mul(p.src[row * p.w + c0 + c], pow2l(tab, p.L1, row));
+            v = fr_mul(p.src[(size_t)row * p.w + c0 + c], pow2l(tab, p.L1, row));
         } else {
-            v = base[row * p.w + c0 + c];
+            v = base[(size_t)row * p.w + c0 + c];
         }
-        lds[(t * G + g) * CW + c] = v;
+        lds[(((t << logG) + g) << LOGCW) + c] = v;
     }
     __syncthreads();
     // ---- k radix-2 stages
@@ -85,27 +96,24 @@ __global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
         const uint32_t s = p.s0 + j;
         const uint32_t logd = DIF ? (p.k - 1 - j) : j;
         const bool trivial = DIF ? (s == p.logH - 1) : (s == 0);
+        const uint32_t dmask = (1u << logd) - 1;
+        // twiddle index of butterfly row i0: DIF (i0 mod H/2^(s+1)) << s, DIT (i0 mod 2^s) << (logH-1-s)
+        const uint32_t tmask = DIF ? (uint32_t)((H >> (s + 1)) - 1) : ((1u << s) - 1);
+        const uint32_t tshift = DIF ? s : (p.logH - 1 - s);
         for (uint32_t bf = threadIdx.x; bf < nbf; bf += blockDim.x) {
-            const uint32_t c = bf % CW;
-            const uint32_t pg = bf / CW;
-            const uint32_t g = pg & (G - 1), pp = pg >> p.logG;
-            const uint32_t t0 = ((pp >> logd) << (logd + 1)) | (pp & ((1u << logd) - 1));
+            const uint32_t c = bf & (CW - 1);
+            const uint32_t pg = bf >> LOGCW;
+            const uint32_t g = pg & (G - 1), pp = pg >> logG;
+            const uint32_t t0 = ((pp >> logd) << (logd + 1)) | (pp & dmask);
             const uint32_t t1 = t0 + (1u << logd);
-            const uint32_t a0 = (t0 * G + g) * CW + c, a1 = (t1 * G + g) * CW + c;
+            const uint32_t a0 = (((t0 << logG) + g) << LOGCW) + c, a1 = (((t1 << logG) + g) << LOGCW) + c;
             const Fr a = lds[a0], b = lds[a1];
             if (trivial) {
                 lds[a0] = fr_add(a, b);
                 lds[a1] = fr_sub(a, b);
                 continue;
             }
-            const uint64_t gid = tile * G + g;
-            const uint64_t i0 = ((gid >> p.logL) << (p.logL + p.k)) + ((uint64_t)t0 << p.logL) + (gid & Lmask);
-            uint64_t twi;
-            if (DIF)
-                twi = (i0 & ((H >> (s + 1)) - 1)) << s;
-            else
-                twi = (i0 & ((1ull << s) - 1)) << (p.logH - 1 - s);
-            const Fr wv = p.tw[twi];
+            const Fr wv = p.tw[(row_of(t0, g) & tmask) << tshift];
             if (DIF) {
                 lds[a0] = fr_add(a, b);
                 lds[a1] = fr_mul(fr_sub(a, b), wv);
@@ -119,20 +127,10 @@ __global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
     }
     // ---- store
     for (uint32_t e = threadIdx.x; e < n_el; e += blockDim.x) {
-        const uint32_t c = e % CW;
-        const uint32_t tg = e / CW;
-        uint32_t t, g;
-        if (t_minor) {
-            t = tg & (K - 1);
-            g = tg >> p.k;
-        } else {
-            t = tg >> p.logG;
-            g = tg & (G - 1);
-        }
+        uint32_t t, g, c;
+        split(e, t, g, c);
         if (c >= cw) continue;
-        const uint64_t gid = tile * G + g;
-        const uint64_t row = ((gid >> p.logL) << (p.logL + p.k)) + ((uint64_t)t << p.logL) + (gid & Lmask);
-        base[row * p.w + c0 + c] = lds[(t * G + g) * CW + c];
+        base[(size_t)row_of(t, g) * p.w + c0 + c] = lds[(((t << logG) + g) << LOGCW) + c];
     }
 }
 
@@ -174,10 +172,11 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
                       const Fr* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
                       hipStream_t st) {
     if (w == 0) return hipSuccess;
-    const uint32_t CW = (uint32_t)(w < 8 ? w : 8);
-    const uint32_t Gmax = 8 / CW;
-    uint32_t logGmax = 0;
-    while ((2u << logGmax) <= Gmax) ++logGmax;
+    // column chunk: the power of two >= min(w, 8); CW * G = 8 (256-byte row runs)
+    uint32_t logCW = 0;
+    while ((1u << logCW) < w && logCW < 3) ++logCW;
+    const uint32_t CW = 1u << logCW;
+    const uint32_t logGmax = 3 - logCW;
     const uint32_t nchunk = (uint32_t)((w + CW - 1) / CW);
     // k <= log2(2048 / (CW * G)) with CW * G <= 8
     const uint32_t kmax = 8;
@@ -201,23 +200,34 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
             p.k = k;
             p.logL = dif ? (logh - s0 - k) : s0;
             p.logG = logG;
-            p.CW = CW;
             p.w = (uint32_t)w;
+            p.nchunk = nchunk;
             p.narr = narr;
             const uint64_t tiles = (uint64_t)narr * ((1ull << logh) >> (k + logG)) * nchunk;
             const size_t lds = (size_t(1) << (k + logG)) * CW * sizeof(Fr);
             const int mode = q == 0 ? first_mode : PASS_INPLACE;
+            const dim3 grid((unsigned)tiles), blk(256);
+#define LSP_NTT_LAUNCH(DIFV, MODEV)                                                                   \
+    switch (logCW) {                                                                                  \
+        case 0: hipLaunchKernelGGL((k_ntt_rm<DIFV, MODEV, 0>), grid, blk, lds, st, p); break;         \
+        case 1: hipLaunchKernelGGL((k_ntt_rm<DIFV, MODEV, 1>), grid, blk, lds, st, p); break;         \
+        case 2: hipLaunchKernelGGL((k_ntt_rm<DIFV, MODEV, 2>), grid, blk, lds, st, p); break;         \
+        default: hipLaunchKernelGGL((k_ntt_rm<DIFV, MODEV, 3>), grid, blk, lds, st, p); break;        \
+    }
             if (dif) {
-                if (mode == PASS_FWD_FIRST)
-                    hipLaunchKernelGGL((k_ntt_rm<true, PASS_FWD_FIRST>), dim3((unsigned)tiles), dim3(256), lds, st, p);
-                else
-                    hipLaunchKernelGGL((k_ntt_rm<true, PASS_INPLACE>), dim3((unsigned)tiles), dim3(256), lds, st, p);
+                if (mode == PASS_FWD_FIRST) {
+                    LSP_NTT_LAUNCH(true, PASS_FWD_FIRST)
+                } else {
+                    LSP_NTT_LAUNCH(true, PASS_INPLACE)
+                }
             } else {
-                if (mode == PASS_INV_FIRST)
-                    hipLaunchKernelGGL((k_ntt_rm<false, PASS_INV_FIRST>), dim3((unsigned)tiles), dim3(256), lds, st, p);
-                else
-                    hipLaunchKernelGGL((k_ntt_rm<false, PASS_INPLACE>), dim3((unsigned)tiles), dim3(256), lds, st, p);
+                if (mode == PASS_INV_FIRST) {
+                    LSP_NTT_LAUNCH(false, PASS_INV_FIRST)
+                } else {
+                    LSP_NTT_LAUNCH(false, PASS_INPLACE)
+                }
             }
+#undef LSP_NTT_LAUNCH
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
             s0 += k;

@@ -333,10 +333,20 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         std::vector<Fr> zh(q), izh(q);
         if (row0 < Q) {
             const uint64_t i0 = host_bitrev(g, logGq);
-            Fr* den = ctx->fbuf("q_den", Sq);
-            Fr* inv_den = ctx->fbuf("q_invden", Sq);
-            LSP_HIP(launch_selector_denoms(tabQ, L1Q, GEN, wh_inv, Sq, den, st, i0, logGq));
-            LSP_HIP(launch_batch_inverse(den, inv_den, Sq, st));
+            // 1/((x-1)(x-w_h^-1)) depends on the domain only: cached per shape in the context
+            char key[64];
+            std::snprintf(key, sizeof key, "qsel_%u_%u_%llu_%u", log_h, logQ, (unsigned long long)i0, logGq);
+            Fr* inv_den;
+            auto it = ctx->ptabs.find(key);
+            if (it != ctx->ptabs.end()) {
+                inv_den = const_cast<Fr*>(it->second);
+            } else {
+                Fr* den = ctx->fbuf("q_den", Sq);
+                inv_den = ctx->fbuf(key, Sq);
+                LSP_HIP(launch_selector_denoms(tabQ, L1Q, GEN, wh_inv, Sq, den, st, i0, logGq));
+                LSP_HIP(launch_batch_inverse(den, inv_den, Sq, st));
+                ctx->ptabs[key] = inv_den;
+            }
             {
                 const Fr gh = fr_pow_u64(GEN, h), gq = host_two_adic_generator(log_q);
                 Fr x = one;

@@ -71,6 +71,24 @@ __global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
             g = tg & (G - 1);
         }
     };
+    // ---- twist factors s^row / h, once per row when every column shares the shift
+    Fr* fac = lds + n_el;  // K * G extra entries (launcher sizes the LDS for it)
+    const bool row_twist = MODE == PASS_FWD_FIRST && !p.twist_per_col;
+    if (row_twist) {
+        const Fr* tab = p.twist + (size_t)arr * ((1ull << p.L1) + (1ull << p.L2));
+        for (uint32_t rg = threadIdx.x; rg < (K << logG); rg += blockDim.x) {
+            uint32_t t, g;
+            if (t_minor) {
+                t = rg & (K - 1);
+                g = rg >> p.k;
+            } else {
+                t = rg >> logG;
+                g = rg & (G - 1);
+            }
+            fac[(t << logG) + g] = pow2l(tab, p.L1, row_of(t, g));
+        }
+        __syncthreads();
+    }
     // ---- load (optionally gathering / twisting)
     for (uint32_t e = threadIdx.x; e < n_el; e += blockDim.x) {
         uint32_t t, g, c;
@@ -81,9 +99,14 @@ __global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
         if (MODE == PASS_INV_FIRST) {
             v = p.src[(size_t)brev_bits(row, p.logH) * p.w + c0 + c];
         } else if (MODE == PASS_FWD_FIRST) {
-            const size_t ti = p.twist_per_col ? ((size_t)arr * p.w + c0 + c) : arr;
-            const Fr* tab = p.twist + ti * ((1ull << p.L1) + (1ull << p.L2));
-            v = fr_mul(p.src[(size_t)row * p.w + c0 + c], pow2l(tab, p.L1, row));
+            Fr f;
+            if (row_twist) {
+                f = fac[(t << logG) + g];
+            } else {
+                const Fr* tab = p.twist + ((size_t)arr * p.w + c0 + c) * ((1ull << p.L1) + (1ull << p.L2));
+                f = pow2l(tab, p.L1, row);
+            }
+            v = fr_mul(p.src[(size_t)row * p.w + c0 + c], f);
         } else {
             v = base[(size_t)row * p.w + c0 + c];
         }
@@ -204,7 +227,8 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
             p.nchunk = nchunk;
             p.narr = narr;
             const uint64_t tiles = (uint64_t)narr * ((1ull << logh) >> (k + logG)) * nchunk;
-            const size_t lds = (size_t(1) << (k + logG)) * CW * sizeof(Fr);
+            // tile, plus one twist factor per row in the first forward pass
+            const size_t lds = ((size_t(1) << (k + logG)) * CW + (size_t(1) << (k + logG))) * sizeof(Fr);
             const int mode = q == 0 ? first_mode : PASS_INPLACE;
             const dim3 grid((unsigned)tiles), blk(256);
 #define LSP_NTT_LAUNCH(DIFV, MODEV)                                                                   \

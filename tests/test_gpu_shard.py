@@ -85,3 +85,16 @@ def test_group_rejects_too_many_ranks(gpu_ctx):
     grp, _ = _group(gpu_ctx, 16)
     with pytest.raises(RuntimeError, match="at most 2\\^log_blowup"):
         grp.prove(tr, permutation_air(3), np.concatenate([a, d]))
+
+
+def test_group_large_equals_single(gpu_ctx):
+    """2^20 rows over 8 virtual ranks (default FRI slice threshold: sharded
+    rounds down to 8K-element slices, then replicated)"""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import gen_permutation_trace
+    a, d, _ = gpu_ctx.config.seeded()
+    tr = gen_permutation_trace(20, 3, a, d)
+    pub = np.concatenate([a, d])
+    single = gpu_ctx.prove(tr, permutation_air(3), pub)
+    grp, _ = _group(gpu_ctx, 8)
+    assert grp.prove(tr, permutation_air(3), pub) == single

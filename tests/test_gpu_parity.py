@@ -309,3 +309,15 @@ def test_prove_with_pow_grinding_matches_oracle(oracle_lib, bits):
     exp = oracle_lib.prove(p, trace.ctypes.data, 32, w, oracle_lib.perm_air(3), fri=fri)
     assert got == exp
     assert oracle_lib.verify(p, got, oracle_lib.perm_air(3), fri=fri) == 0
+
+
+@pytest.mark.parametrize("logn,ncols", [(16, 3), (15, 6)])
+def test_prove_bit_exact_vs_oracle_large(gpu_ctx, oracle_lib, logn, ncols):
+    """Full proofs at 2^15-2^16 rows against the multithreaded C oracle (a few
+    seconds on the host): every stage at the sizes where the GPU kernels take
+    their wide (non-cooperative, multi-pass) paths."""
+    from linea_stark_prover_amd.air import permutation_air
+    s, p, trace, w = _perm_setup(logn, ncols, oracle_lib)
+    got = gpu_ctx.prove(trace, permutation_air(ncols), _pub(p))
+    exp = oracle_lib.prove(p, trace.ctypes.data, 1 << logn, w, oracle_lib.perm_air(ncols))
+    assert got == exp

@@ -17,3 +17,13 @@ def test_wide_prove_matches_oracle(gpu_ctx, oracle_lib, log_n, shape):
     p = oracle_lib.setup()
     exp = oracle_lib.prove(p, tr.ctypes.data, 1 << log_n, tr.shape[1], air.descriptor())
     assert got == exp
+
+
+def test_wide_prove_matches_oracle_2e12(gpu_ctx, oracle_lib):
+    from linea_stark_prover_amd.prover import gen_wide_trace
+    a, d, _ = gpu_ctx.config.seeded()
+    tr, air = gen_wide_trace(12, a, d)  # the C3 shape: 4 lookups + 8 groups of 6+6, W = 184
+    pub = np.concatenate([a, d])
+    got = gpu_ctx.prove(tr, air, pub)
+    p = oracle_lib.setup()
+    assert got == oracle_lib.prove(p, tr.ctypes.data, 1 << 12, tr.shape[1], air.descriptor())

@@ -187,11 +187,26 @@ __device__ __forceinline__ F29 f29_const(uint32_t l0, uint32_t l1, uint32_t l2, 
     return o;
 }
 
-// ark-ff Montgomery (x 2^256) -> F29 (x 2^261): times 2^5 via a product by 2^266 mod r
+// ark-ff Montgomery (X = x 2^256 mod r, < 2^256) -> F29 (x 2^261): the integer
+// X * 2^5 (< 32 r < 2^261) is already a lazily reduced F29 value, so this is a
+// repack with a 5-bit offset plus one cheap reduction to < 2r -- no product.
 __device__ __forceinline__ F29 f29_from_fr(const Fr& x) {
-    const F29 c = f29_const(0x1fffc927u, 0x1153ffffu, 0x1ff1bfb1u, 0xec4435fu, 0x185f1096u, 0x1ce80ad5u,
-                            0x587fb98u, 0x93ca8f4u, 0x5551eu);
-    return f29_mul(f29_repack_in(x), c);
+    F29 o;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const int bit = 29 * i - 5;  // limb i of X << 5 = bits [29 i - 5, 29 i + 24) of X
+        uint32_t v;
+        if (bit < 0) {
+            v = x.v[0] << 5;
+        } else {
+            const int w = bit >> 5, sh = bit & 31;
+            uint64_t t = x.v[w];
+            if (w + 1 < 8) t |= (uint64_t)x.v[w + 1] << 32;
+            v = (uint32_t)(t >> sh);
+        }
+        o.l[i] = v & (i < 8 ? F29_MASK : 0xffffffffu);
+    }
+    return f29_reduce(o);
 }
 
 // F29 -> canonical ark-ff Montgomery words: times 2^-5 (product by 2^256 mod r), reduce to [0, r)

@@ -1,11 +1,16 @@
 // Poseidon2Bls12337<3> on the 29-bit-limb representation (fr29.hpp).
 // Same permutation as poseidon2.hpp (U1-U3 conventions); only the arithmetic
-// representation differs.  Lazy-reduction bounds (r = the field modulus):
-//   S-box inputs < 32 r (f29_mul requirement), outputs < 3.3 r;
-//   full rounds: state < 5.5 r after the external layer;
-//   partial rounds: t = reduce(s0 + s1 + s2) < 2 r, s2 reduced every round
-//   (it doubles), s1 grows by < 2 r per round and is reduced once after the
-//   partial rounds (< 50 r < 2^259 in between).
+// representation differs.  Lazy-reduction bounds (r = the field modulus;
+// "normalised" = limbs 0..7 < 2^29):
+//   products: inputs < 32 r with limbs < 2^30; output normalised and
+//     < 1 + 0.0023 K^2 r for inputs < K r, so an S-box output is < 1.04 r;
+//   the external layer's t = s0 + s1 + s2 is a limb-wise sum (limbs < 3 2^29,
+//     no carries) and is folded into the next S-box input together with the
+//     round constant by one carry-propagating add: inputs < 14.8 r;
+//   partial rounds: t = reduce(s0 + s1 + s2) < 2 r, s2 = reduce(2 s2 + t)
+//     (limb-wise sums into f29_reduce, which normalises any limbs < 2^32),
+//     s1 grows by < 2 r per round and is reduced after the partial rounds;
+//   the output state is normalised and < 4.2 r.
 #pragma once
 #include "fr29.hpp"
 
@@ -20,11 +25,26 @@ __device__ __forceinline__ F29 sbox29(const F29& x) {
     return f29_mul(f29_sqr(x8), x);  // x^17
 }
 
-__device__ __forceinline__ void ext_layer29(F29& s0, F29& s1, F29& s2) {
-    const F29 t = f29_add(f29_add(s0, s1), s2);
-    s0 = f29_add(s0, t);
-    s1 = f29_add(s1, t);
-    s2 = f29_add(s2, t);
+__device__ __forceinline__ F29 f29_zero() {
+    F29 z;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) z.l[i] = 0;
+    return z;
+}
+
+// limb-wise sums without carry propagation (see the bounds above)
+__device__ __forceinline__ F29 f29_lazy2(const F29& a, const F29& b) {
+    F29 o;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o.l[i] = a.l[i] + b.l[i];
+    return o;
+}
+
+__device__ __forceinline__ F29 f29_lazy3(const F29& a, const F29& b, const F29& c) {
+    F29 o;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o.l[i] = a.l[i] + b.l[i] + c.l[i];
+    return o;
 }
 
 // rc29: round constants in F29 form, new_from_rng order (initial external
@@ -36,29 +56,37 @@ __device__ __forceinline__ void permute3_f29(F29& s0, F29& s1, F29& s2, const F2
     const F29* ini = rc29;
     const F29* ter = rc29 + 3 * half;
     const F29* itl = rc29 + 6 * half;
-    ext_layer29(s0, s1, s2);
+    // t: the pending external layer (s_i + t), applied at the next S-box input
+    F29 t = f29_lazy3(s0, s1, s2);
     for (uint32_t r = 0; r < half; ++r) {
-        s0 = sbox29<D>(f29_add(s0, ini[3 * r + 0]));
-        s1 = sbox29<D>(f29_add(s1, ini[3 * r + 1]));
-        s2 = sbox29<D>(f29_add(s2, ini[3 * r + 2]));
-        ext_layer29(s0, s1, s2);
+        s0 = sbox29<D>(f29_add(f29_lazy2(s0, ini[3 * r + 0]), t));
+        s1 = sbox29<D>(f29_add(f29_lazy2(s1, ini[3 * r + 1]), t));
+        s2 = sbox29<D>(f29_add(f29_lazy2(s2, ini[3 * r + 2]), t));
+        t = f29_lazy3(s0, s1, s2);
     }
-    s1 = f29_reduce(s1);
-    s2 = f29_reduce(s2);
+    // x: the next partial-round S-box input (s0 + round constant)
+    F29 x = rp ? f29_add(f29_lazy2(s0, itl[0]), t) : f29_add(s0, t);
+    s1 = f29_reduce(f29_lazy2(s1, t));
+    s2 = f29_reduce(f29_lazy2(s2, t));
     for (uint32_t r = 0; r < rp; ++r) {
-        s0 = sbox29<D>(f29_add(s0, itl[r]));
-        const F29 t = f29_reduce(f29_add(f29_add(s0, s1), s2));
-        s0 = f29_add(s0, t);
-        s1 = f29_add(s1, t);
-        s2 = f29_reduce(f29_add(f29_add(s2, s2), t));
+        const F29 y = sbox29<D>(x);
+        const F29 u = f29_reduce(f29_lazy3(y, s1, s2));
+        s1 = f29_add(s1, u);
+        s2 = f29_reduce(f29_lazy3(s2, s2, u));
+        x = r + 1 < rp ? f29_add(f29_lazy2(y, itl[r + 1]), u) : f29_add(y, u);
     }
+    s0 = x;
     s1 = f29_reduce(s1);
+    t = f29_zero();
     for (uint32_t r = 0; r < half; ++r) {
-        s0 = sbox29<D>(f29_add(s0, ter[3 * r + 0]));
-        s1 = sbox29<D>(f29_add(s1, ter[3 * r + 1]));
-        s2 = sbox29<D>(f29_add(s2, ter[3 * r + 2]));
-        ext_layer29(s0, s1, s2);
+        s0 = sbox29<D>(f29_add(f29_lazy2(s0, ter[3 * r + 0]), t));
+        s1 = sbox29<D>(f29_add(f29_lazy2(s1, ter[3 * r + 1]), t));
+        s2 = sbox29<D>(f29_add(f29_lazy2(s2, ter[3 * r + 2]), t));
+        t = f29_lazy3(s0, s1, s2);
     }
+    s0 = f29_add(s0, t);
+    s1 = f29_add(s1, t);
+    s2 = f29_add(s2, t);
 }
 
 // ---- quad-cooperative permutation, for launches narrower than the chip.
@@ -88,16 +116,40 @@ __device__ __forceinline__ F29 f29_sel3(uint32_t j, const F29& a, const F29& b, 
     return r;
 }
 
+// one full round on a quad, with the pending external layer t of the
+// previous round folded into the S-box input; returns the new pending t
 template <uint32_t D>
-__device__ __forceinline__ void full_round_coop(F29& s0, F29& s1, F29& s2, const F29* __restrict__ c, uint32_t j) {
-    const F29 x = sbox29<D>(f29_sel3(j, f29_add(s0, c[0]), f29_add(s1, c[1]), f29_add(s2, c[2])));
+__device__ __forceinline__ F29 full_round_coop(F29& s0, F29& s1, F29& s2, const F29& t, const F29* __restrict__ c,
+                                               uint32_t j) {
+    const F29 in = f29_sel3(j, f29_lazy2(s0, c[0]), f29_lazy2(s1, c[1]), f29_lazy2(s2, c[2]));
+    const F29 x = sbox29<D>(f29_add(in, t));
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
         s0.l[i] = quad_bcast(x.l[i], 0);
         s1.l[i] = quad_bcast(x.l[i], 1);
         s2.l[i] = quad_bcast(x.l[i], 2);
     }
-    ext_layer29(s0, s1, s2);
+    return f29_lazy3(s0, s1, s2);
+}
+
+// partial-round S-box on a quad: x^11 = x^8 x^3 with x^4 (lane 0) and x^3
+// (lane 1) in parallel after x^2 -- four sequential products instead of five
+template <uint32_t D>
+__device__ __forceinline__ F29 sbox29_coop(const F29& x) {
+    if (D != 11) return sbox29<D>(x);
+    const F29 x2 = f29_sqr(x);
+    const uint32_t odd = 0u - (threadIdx.x & 1u);
+    F29 sel;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) sel.l[i] = (x.l[i] & odd) | (x2.l[i] & ~odd);
+    const F29 y = f29_mul(x2, sel);  // lane 0: x^4, lane 1: x^3
+    F29 x4, x3;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        x4.l[i] = quad_bcast(y.l[i], 0);
+        x3.l[i] = quad_bcast(y.l[i], 1);
+    }
+    return f29_mul(f29_sqr(x4), x3);
 }
 
 template <uint32_t D>
@@ -108,26 +160,25 @@ __device__ __forceinline__ void permute3_f29_coop(F29& s0, F29& s1, F29& s2, con
     const F29* ini = rc29;
     const F29* ter = rc29 + 3 * half;
     const F29* itl = rc29 + 6 * half;
-    ext_layer29(s0, s1, s2);
-    for (uint32_t r = 0; r < half; ++r) full_round_coop<D>(s0, s1, s2, ini + 3 * r, j);
-    s1 = f29_reduce(s1);
-    s2 = f29_reduce(s2);
+    F29 t = f29_lazy3(s0, s1, s2);
+    for (uint32_t r = 0; r < half; ++r) t = full_round_coop<D>(s0, s1, s2, t, ini + 3 * r, j);
+    F29 x = rp ? f29_add(f29_lazy2(s0, itl[0]), t) : f29_add(s0, t);
+    s1 = f29_reduce(f29_lazy2(s1, t));
+    s2 = f29_reduce(f29_lazy2(s2, t));
     for (uint32_t r = 0; r < rp; ++r) {
-        s0 = sbox29<D>(f29_add(s0, itl[r]));
-        const F29 t = f29_reduce(f29_add(f29_add(s0, s1), s2));
-        s0 = f29_add(s0, t);
-        s1 = f29_add(s1, t);
-        s2 = f29_reduce(f29_add(f29_add(s2, s2), t));
+        const F29 y = sbox29_coop<D>(x);
+        const F29 u = f29_reduce(f29_lazy3(y, s1, s2));
+        s1 = f29_add(s1, u);
+        s2 = f29_reduce(f29_lazy3(s2, s2, u));
+        x = r + 1 < rp ? f29_add(f29_lazy2(y, itl[r + 1]), u) : f29_add(y, u);
     }
+    s0 = x;
     s1 = f29_reduce(s1);
-    for (uint32_t r = 0; r < half; ++r) full_round_coop<D>(s0, s1, s2, ter + 3 * r, j);
-}
-
-__device__ __forceinline__ F29 f29_zero() {
-    F29 z;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) z.l[i] = 0;
-    return z;
+    t = f29_zero();
+    for (uint32_t r = 0; r < half; ++r) t = full_round_coop<D>(s0, s1, s2, t, ter + 3 * r, j);
+    s0 = f29_add(s0, t);
+    s1 = f29_add(s1, t);
+    s2 = f29_add(s2, t);
 }
 
 template <uint32_t D, bool COOP = false>

@@ -8,9 +8,9 @@
 //
 // Representation: x is held as X = x * 2^261 mod r ("Montgomery, R' = 2^261")
 // in limbs l[0..8] of 29 bits (l[8] may hold a few more bits).  Values are
-// kept lazily reduced; the invariants (see fr29_mul) are
-//   mul inputs  < 32 r with normalised limbs  ->  mul output < 3.3 r,
-// and values < 8 r whenever they come from the adders below.
+// kept lazily reduced; the invariants (see f29_mul_c) are
+//   mul inputs  < K r (< 2^261) with normalised limbs (limbs 0..7 < 2^29)
+//   ->  mul output normalised and < (8 + 0.0023 K^2) r.
 // Conversions to/from the ark-ff form (x * 2^256 mod r, 8 x 32-bit limbs):
 // from: repack bits, Montgomery-multiply by 2^266 mod r (x 2^5);
 // to:   Montgomery-multiply by 2^256 mod r (x 2^-5), reduce to [0, r), repack.
@@ -44,9 +44,11 @@ __device__ __forceinline__ constexpr uint32_t p29(int i) {
 #define LSP_F29_USE_ASM 1
 #endif
 
-// Montgomery product a * b * 2^-261 mod r (lazy: output < 3.3 r for inputs
-// < 32 r).  FIPS, one 64-bit accumulator; -r^-1 mod 2^29 = 2^29 - 1, so the
-// quotient digit is m = -t mod 2^29, and m * r[0] = m clears the low digit.
+// Montgomery product a * b * 2^-261 mod r.  FIPS, one 64-bit accumulator.
+// r = 1 mod 2^29, so the quotient digit can be m_k = -t mod 2^32 (a full
+// word: no mask) and m_k * r[0] = m_k clears the low 29 bits of the column.
+// Column sums stay < 2^63.2 (tools/gen_fr29mul.py --bound); the quotient
+// M = sum m_k 2^(29k) < 2^264, so the output is < a b / 2^261 + 8 r.
 __device__ __forceinline__ F29 f29_mul_c(const F29& a, const F29& b) {
     uint32_t m[9];
     F29 o;
@@ -59,7 +61,7 @@ __device__ __forceinline__ F29 f29_mul_c(const F29& a, const F29& b) {
             acc += (uint64_t)m[j] * p29(k - j);
         }
         acc += (uint64_t)a.l[k] * b.l[0];
-        m[k] = (0u - (uint32_t)acc) & F29_MASK;
+        m[k] = 0u - (uint32_t)acc;
         acc = (acc + m[k]) >> 29;
     }
 #pragma unroll
@@ -93,7 +95,7 @@ __device__ __forceinline__ F29 f29_sqr_c(const F29& a) {
 #pragma unroll
         for (int j = (k > 8 ? k - 8 : 0); j < (k < 9 ? k : 9); ++j) acc += (uint64_t)m[j] * p29(k - j);
         if (k < 9) {
-            m[k] = (0u - (uint32_t)acc) & F29_MASK;
+            m[k] = 0u - (uint32_t)acc;
             acc = (acc + m[k]) >> 29;
         } else {
             o.l[k - 9] = (uint32_t)acc & F29_MASK;
@@ -213,11 +215,8 @@ __device__ __forceinline__ F29 f29_from_fr(const Fr& x) {
 __device__ __forceinline__ Fr f29_to_fr(const F29& x) {
     const F29 c = f29_const(0x1ffffff3u, 0x8e3ffffu, 0x1ffffc9fu, 0xfea1edfu, 0xfee725u, 0xabaa896u, 0xa745b60u,
                             0x6457773u, 0xd4bdau);
-    F29 y = f29_mul(f29_reduce(x), c);  // < 3.3 r
-    Fr o = f29_repack_out(y);           // < 4r < 2^256
-    o = fr_reduce_once(o);
-    o = fr_reduce_once(o);
-    return fr_reduce_once(o);
+    const F29 y = f29_reduce(f29_mul(f29_reduce(x), c));  // < 2 r
+    return fr_reduce_once(f29_repack_out(y));
 }
 
 }  // namespace lsp

@@ -1,16 +1,18 @@
 // Poseidon2Bls12337<3> on the 29-bit-limb representation (fr29.hpp).
 // Same permutation as poseidon2.hpp (U1-U3 conventions); only the arithmetic
 // representation differs.  Lazy-reduction bounds (r = the field modulus;
-// "normalised" = limbs 0..7 < 2^29):
-//   products: inputs < 32 r with limbs < 2^30; output normalised and
-//     < 1 + 0.0023 K^2 r for inputs < K r, so an S-box output is < 1.04 r;
-//   the external layer's t = s0 + s1 + s2 is a limb-wise sum (limbs < 3 2^29,
-//     no carries) and is folded into the next S-box input together with the
-//     round constant by one carry-propagating add: inputs < 14.8 r;
+// "normalised" = limbs 0..7 < 2^29; a product of inputs < K r is normalised
+// and < (8 + 0.0023 K^2) r, fr29.hpp):
+//   S-box inputs are normalised (one carry-propagating add) and < 86 r
+//     (< 2^259), outputs < 9.7 r (fixed point of the bounds below);
+//   the external layer's t = s0 + s1 + s2 is a limb-wise sum (no carries)
+//     folded into the next S-box input with the round constant: inputs
+//     < 4 Y + 2 inside a permutation (Y = the S-box output bound), < 8 Y + 6
+//     at the start of a sponge permutation (s2 carries over);
 //   partial rounds: t = reduce(s0 + s1 + s2) < 2 r, s2 = reduce(2 s2 + t)
-//     (limb-wise sums into f29_reduce, which normalises any limbs < 2^32),
+//     (limb-wise sums into f29_reduce, which normalises limbs < 2^32),
 //     s1 grows by < 2 r per round and is reduced after the partial rounds;
-//   the output state is normalised and < 4.2 r.
+//   the output state is normalised and < 4 Y.
 #pragma once
 #include "fr29.hpp"
 

@@ -187,6 +187,8 @@ int lsp_ctx_destroy(lsp_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (auto& kv : ctx->pool)
         if (kv.second.p) (void)hipFree(kv.second.p);
+    for (auto& kv : ctx->hpool)
+        if (kv.second.p) (void)hipHostFree(kv.second.p);
     for (auto& kv : ctx->twiddles) (void)hipFree(kv.second);
     if (ctx->rc_dev) (void)hipFree(ctx->rc_dev);
     if (ctx->rc29_dev) (void)hipFree(ctx->rc29_dev);

@@ -3,6 +3,7 @@
 #include "host.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 
@@ -62,48 +63,63 @@ HostPool::HostPool(unsigned workers) {
 HostPool::~HostPool() {
     {
         std::lock_guard<std::mutex> lk(m_);
-        stop_ = true;
+        stop_.store(true);
     }
     cv_.notify_all();
     for (auto& t : th_) t.join();
 }
 
+static inline void cpu_relax() {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+}
+
 void HostPool::loop() {
     uint64_t seen = 0;
     for (;;) {
-        const std::function<void(size_t)>* job;
-        size_t n;
-        {
-            std::unique_lock<std::mutex> lk(m_);
-            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-            if (stop_) return;
-            seen = gen_;
-            job = job_;
-            n = n_;
+        // spin for a new generation, then sleep
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned it = 0; gen_.load() == seen && !stop_.load(); ++it) {
+            cpu_relax();
+            if ((it & 255) == 255 &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) {
+                std::unique_lock<std::mutex> lk(m_);
+                sleepers_.fetch_add(1);  // seq_cst: pairs with parallel_for's gen_ / sleepers_ order
+                cv_.wait(lk, [&] { return stop_.load() || gen_.load() != seen; });
+                sleepers_.fetch_sub(1);
+                break;
+            }
         }
+        if (stop_.load()) return;
+        seen = gen_.load();
+        const auto* job = job_;
+        const size_t n = n_;
         for (size_t i; (i = next_.fetch_add(1)) < n;) (*job)(i);
-        std::lock_guard<std::mutex> lk(m_);
-        if (--busy_ == 0) done_.notify_all();
+        busy_.fetch_sub(1);
     }
 }
 
 void HostPool::parallel_for(size_t n, const std::function<void(size_t)>& f) {
-    if (th_.empty() || n < 4) {
+    if (th_.empty() || n < 2) {
         for (size_t i = 0; i < n; ++i) f(i);
         return;
     }
-    {
+    // the previous job has fully drained (busy_ == 0), so no worker reads these
+    job_ = &f;
+    n_ = n;
+    next_.store(0);
+    busy_.store((unsigned)th_.size());
+    gen_.fetch_add(1);
+    if (sleepers_.load() != 0) {
         std::lock_guard<std::mutex> lk(m_);
-        job_ = &f;
-        n_ = n;
-        next_.store(0);
-        busy_ = (unsigned)th_.size();
-        ++gen_;
+        cv_.notify_all();
     }
-    cv_.notify_all();
     for (size_t i; (i = next_.fetch_add(1)) < n;) f(i);
-    std::unique_lock<std::mutex> lk(m_);
-    done_.wait(lk, [&] { return busy_ == 0; });
+    for (unsigned it = 0; busy_.load() != 0; ++it) {
+        cpu_relax();
+        if ((it & 4095) == 4095) std::this_thread::yield();
+    }
 }
 
 Fr P2Host::hash(const Fr* in, size_t n) const {
@@ -264,6 +280,26 @@ void* lsp_ctx::buf(const std::string& name, size_t bytes) {
             if (e != hipSuccess) {
                 (void)hipGetLastError();
                 throw lsp::LspError(LSP_E_OOM, "hipMalloc(" + std::to_string(bytes) + ") for " + name + " failed");
+            }
+            b.cap = bytes;
+        }
+    }
+    return b.p;
+}
+
+void* lsp_ctx::hbuf(const std::string& name, size_t bytes) {
+    Buf& b = hpool[name];
+    if (b.cap < bytes) {
+        if (b.p) {
+            LSP_HIP(hipStreamSynchronize(stream));
+            LSP_HIP(hipHostFree(b.p));
+            b.p = nullptr;
+            b.cap = 0;
+        }
+        if (bytes) {
+            if (hipHostMalloc(&b.p, bytes, hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                throw lsp::LspError(LSP_E_OOM, "hipHostMalloc(" + std::to_string(bytes) + ") for " + name + " failed");
             }
             b.cap = bytes;
         }

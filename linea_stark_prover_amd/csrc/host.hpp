@@ -19,6 +19,7 @@
 #include "fr.hpp"
 #include "kernels.hpp"
 #include "poseidon2.hpp"
+#include "poseidon2_host64.hpp"
 
 namespace lsp {
 
@@ -62,7 +63,8 @@ uint32_t log2_exact(size_t n);  // throws LSP_E_SIZE on non-power-of-two
 struct P2Host {
     P2Layout L;
     std::vector<Fr> rc;
-    void permute(Fr& s0, Fr& s1, Fr& s2) const { permute3_rt(s0, s1, s2, rc.data(), L); }
+    // 4 x 64-bit limbs, lazily reduced (poseidon2_host64.hpp); canonical in and out
+    void permute(Fr& s0, Fr& s1, Fr& s2) const { hp64::permute3_rt(s0, s1, s2, rc.data(), L); }
     Fr hash(const Fr* in, size_t n) const;
     Fr compress(const Fr& l, const Fr& r) const {
         Fr s0 = l, s1 = r, s2 = fr_zero();
@@ -169,25 +171,30 @@ struct Comm;
 
 // Small persistent host thread pool: parallel_for over [0, n) with the
 // calling thread participating.  Used for the Merkle tree tops the prover
-// finishes on the host (a few dozen permutations per level).
+// finishes on the host: 7 back-to-back levels of a few dozen permutations,
+// so a dispatch must cost microseconds, not a condition-variable wake-up per
+// level -- workers spin on the job generation for a short window after each
+// job (kSpinUs) before sleeping, and the caller spins for completion.
 class HostPool {
   public:
     explicit HostPool(unsigned workers);
     ~HostPool();
     void parallel_for(size_t n, const std::function<void(size_t)>& f);
     unsigned size() const { return (unsigned)th_.size() + 1; }
+    static constexpr int kSpinUs = 300;
 
   private:
     void loop();
     std::vector<std::thread> th_;
     std::mutex m_;
-    std::condition_variable cv_, done_;
+    std::condition_variable cv_;
     const std::function<void(size_t)>* job_ = nullptr;
     size_t n_ = 0;
     std::atomic<size_t> next_{0};
-    unsigned busy_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
+    std::atomic<unsigned> busy_{0};
+    std::atomic<unsigned> sleepers_{0};
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<bool> stop_{false};
 };
 }  // namespace lsp
 
@@ -209,12 +216,15 @@ struct lsp_ctx {
         size_t cap = 0;
     };
     std::map<std::string, Buf> pool;
+    std::map<std::string, Buf> hpool;  // pinned host staging buffers (hbuf)
     std::map<std::pair<uint32_t, int>, lsp::Fr*> twiddles;
     std::map<std::string, const lsp::Fr*> ptabs;  // cached power tables (prove.cpp pow_table), pool-owned
     std::vector<std::pair<std::string, double>> timings;
 
     void* buf(const std::string& name, size_t bytes);
     lsp::Fr* fbuf(const std::string& name, size_t n) { return (lsp::Fr*)buf(name, n * sizeof(lsp::Fr)); }
+    // pinned host memory; growing it first drains the stream (a copy may still read it)
+    void* hbuf(const std::string& name, size_t bytes);
     const lsp::Fr* twiddle(uint32_t logH, bool inverse);
     lsp::HostPool& host_pool();
     void sync();

@@ -1,0 +1,164 @@
+// Poseidon2Bls12337<3> on the host, in 4 x 64-bit limbs: the permutation the
+// host runs on the critical path (Merkle tree tops, the challenger's sponge).
+// Same function as permute3 (poseidon2.hpp, U1-U3 conventions) and the same
+// in-memory element form (ark-ff Montgomery, R = 2^256: an Fr's eight 32-bit
+// words are these four 64-bit limbs), but values stay lazily reduced in
+// [0, 2r) between operations:
+//   * product: CIOS without the final subtraction -- for inputs < 2r the
+//     output is < 4r^2/2^256 + r < 1.3 r (r < 2^252.3);
+//   * sum: a + b < 4r < 2^255, then one conditional subtraction of 2r;
+//   * the permutation's outputs are made canonical ([0, r)) at the end.
+#pragma once
+#include <stdint.h>
+
+#include "poseidon2.hpp"
+
+namespace lsp {
+namespace hp64 {
+
+typedef unsigned __int128 u128;
+struct F {
+    uint64_t l[4];
+};
+
+// (host-only functions; the constants are spelled out so the header also
+// parses in the device compilation pass)
+constexpr uint64_t R0 = (uint64_t)LSP_MOD0 | ((uint64_t)LSP_MOD1 << 32), R1 = (uint64_t)LSP_MOD2 | ((uint64_t)LSP_MOD3 << 32),
+                   R2 = (uint64_t)LSP_MOD4 | ((uint64_t)LSP_MOD5 << 32), R3 = (uint64_t)LSP_MOD6 | ((uint64_t)LSP_MOD7 << 32);
+constexpr uint64_t inv64() {  // r^-1 mod 2^64 (Newton)
+    uint64_t x = 1;
+    for (int i = 0; i < 7; ++i) x *= 2 - R0 * x;
+    return x;
+}
+constexpr uint64_t NP = 0 - inv64();  // -r^-1 mod 2^64
+// 2r
+constexpr uint64_t D0 = R0 << 1, D1 = (R1 << 1) | (R0 >> 63), D2 = (R2 << 1) | (R1 >> 63), D3 = (R3 << 1) | (R2 >> 63);
+
+inline F from(const Fr& x) {
+    F o;
+    __builtin_memcpy(o.l, x.v, 32);
+    return o;
+}
+
+// a - m if a >= m, else a (m = the 4-limb constant)
+inline F csub(const F& a, uint64_t m0, uint64_t m1, uint64_t m2, uint64_t m3) {
+    uint64_t d[4];
+    u128 v = (u128)a.l[0] - m0;
+    d[0] = (uint64_t)v;
+    v = (u128)a.l[1] - m1 - (uint64_t)((v >> 64) & 1);
+    d[1] = (uint64_t)v;
+    v = (u128)a.l[2] - m2 - (uint64_t)((v >> 64) & 1);
+    d[2] = (uint64_t)v;
+    v = (u128)a.l[3] - m3 - (uint64_t)((v >> 64) & 1);
+    d[3] = (uint64_t)v;
+    const uint64_t keep = 0 - (uint64_t)((v >> 64) & 1);  // borrow: a < m
+    F o;
+    for (int i = 0; i < 4; ++i) o.l[i] = (a.l[i] & keep) | (d[i] & ~keep);
+    return o;
+}
+
+inline Fr to_canonical(const F& x) {
+    const F c = csub(x, R0, R1, R2, R3);
+    Fr o;
+    __builtin_memcpy(o.v, c.l, 32);
+    return o;
+}
+
+inline F add(const F& a, const F& b) {
+    F s;
+    u128 c = (u128)a.l[0] + b.l[0];
+    s.l[0] = (uint64_t)c;
+    c = (u128)a.l[1] + b.l[1] + (uint64_t)(c >> 64);
+    s.l[1] = (uint64_t)c;
+    c = (u128)a.l[2] + b.l[2] + (uint64_t)(c >> 64);
+    s.l[2] = (uint64_t)c;
+    s.l[3] = a.l[3] + b.l[3] + (uint64_t)(c >> 64);
+    return csub(s, D0, D1, D2, D3);
+}
+
+inline F mul(const F& a, const F& b) {
+    uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+    for (int i = 0; i < 4; ++i) {
+        const uint64_t y = b.l[i];
+        u128 c = (u128)a.l[0] * y + t0;
+        t0 = (uint64_t)c;
+        c = (u128)a.l[1] * y + t1 + (uint64_t)(c >> 64);
+        t1 = (uint64_t)c;
+        c = (u128)a.l[2] * y + t2 + (uint64_t)(c >> 64);
+        t2 = (uint64_t)c;
+        c = (u128)a.l[3] * y + t3 + (uint64_t)(c >> 64);
+        t3 = (uint64_t)c;
+        t4 += (uint64_t)(c >> 64);
+        const uint64_t m = t0 * NP;
+        c = (u128)m * R0 + t0;
+        c = (u128)m * R1 + t1 + (uint64_t)(c >> 64);
+        t0 = (uint64_t)c;
+        c = (u128)m * R2 + t2 + (uint64_t)(c >> 64);
+        t1 = (uint64_t)c;
+        c = (u128)m * R3 + t3 + (uint64_t)(c >> 64);
+        t2 = (uint64_t)c;
+        c = (u128)t4 + (uint64_t)(c >> 64);
+        t3 = (uint64_t)c;
+        t4 = (uint64_t)(c >> 64);
+    }
+    return F{{t0, t1, t2, t3}};
+}
+
+template <uint32_t D>
+inline F sbox(const F& x) {
+    const F x2 = mul(x, x);
+    const F x4 = mul(x2, x2);
+    const F x8 = mul(x4, x4);
+    if (D == 11) return mul(mul(x8, x2), x);
+    return mul(mul(x8, x8), x);  // x^17
+}
+
+inline void ext_layer(F& s0, F& s1, F& s2) {
+    const F t = add(add(s0, s1), s2);
+    s0 = add(s0, t);
+    s1 = add(s1, t);
+    s2 = add(s2, t);
+}
+
+// rc: constants in new_from_rng order (poseidon2.hpp); states in and out canonical
+template <uint32_t D>
+inline void permute3(Fr& a0, Fr& a1, Fr& a2, const Fr* rc, uint32_t rounds_f, uint32_t rounds_p) {
+    const uint32_t half = rounds_f / 2;
+    const Fr* ini = rc;
+    const Fr* ter = rc + 3 * half;
+    const Fr* itl = rc + 6 * half;
+    F s0 = from(a0), s1 = from(a1), s2 = from(a2);
+    ext_layer(s0, s1, s2);
+    for (uint32_t r = 0; r < half; ++r) {
+        s0 = sbox<D>(add(s0, from(ini[3 * r + 0])));
+        s1 = sbox<D>(add(s1, from(ini[3 * r + 1])));
+        s2 = sbox<D>(add(s2, from(ini[3 * r + 2])));
+        ext_layer(s0, s1, s2);
+    }
+    for (uint32_t r = 0; r < rounds_p; ++r) {
+        s0 = sbox<D>(add(s0, from(itl[r])));
+        const F t = add(add(s0, s1), s2);
+        s0 = add(s0, t);
+        s1 = add(s1, t);
+        s2 = add(add(s2, s2), t);
+    }
+    for (uint32_t r = 0; r < half; ++r) {
+        s0 = sbox<D>(add(s0, from(ter[3 * r + 0])));
+        s1 = sbox<D>(add(s1, from(ter[3 * r + 1])));
+        s2 = sbox<D>(add(s2, from(ter[3 * r + 2])));
+        ext_layer(s0, s1, s2);
+    }
+    a0 = to_canonical(s0);
+    a1 = to_canonical(s1);
+    a2 = to_canonical(s2);
+}
+
+inline void permute3_rt(Fr& s0, Fr& s1, Fr& s2, const Fr* rc, const P2Layout& L) {
+    if (L.sbox_degree == 17)
+        permute3<17>(s0, s1, s2, rc, L.rounds_f, L.rounds_p);
+    else
+        permute3<11>(s0, s1, s2, rc, L.rounds_f, L.rounds_p);
+}
+
+}  // namespace hp64
+}  // namespace lsp

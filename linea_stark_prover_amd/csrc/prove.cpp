@@ -134,24 +134,26 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
 // MerkleTreeMmcs::commit of `m` into `layers` (2*height - 1 digests, leaves
 // first).  Wide levels run on the GPU; once a layer has at most
 // host_tree_top digests the remaining levels are a few dozen permutations on
-// the critical path, and the host (a ~40 ns multiply chain against ~470 ns
-// for one wave's multiply) finishes them with a small thread pool.  Trees of
+// the critical path, and the host (a ~30 ns multiply against ~350 ns for one
+// wave's multiply chain) finishes them with a small thread pool.  Trees of
 // at most host_tree_top single-matrix rows are hashed on the host entirely.
-// The host layers are copied back so openings gather from device memory.
+// The host layers go back to the device (openings gather from device memory)
+// from a pinned staging buffer, without waiting: the next use of the buffer
+// comes after a later synchronisation of the same stream.
 Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers) {
     hipStream_t st = ctx->stream;
     size_t top = ctx->host_tree_top;
     if (const char* e = std::getenv("LSP_HOST_TREE_TOP")) top = std::strtoull(e, nullptr, 10);
     HostPool& pool = ctx->host_pool();
-    std::vector<Fr> host;  // host layers, starting at device offset `off`
     size_t off = 0, len = height;
     const bool leaves_on_host = height <= top && m.n == 1 && height > 1;
+    Fr* host;  // host layers, starting at device offset `off` (pinned)
     if (leaves_on_host) {
         const size_t w = m.width[0];
-        std::vector<Fr> rows(height * w);
-        LSP_HIP(hipMemcpyAsync(rows.data(), m.ptr[0], rows.size() * sizeof(Fr), hipMemcpyDeviceToHost, st));
+        host = (Fr*)ctx->hbuf("merkle_top", (2 * height - 1 + height * w) * sizeof(Fr));
+        Fr* rows = host + 2 * height - 1;
+        LSP_HIP(hipMemcpyAsync(rows, m.ptr[0], height * w * sizeof(Fr), hipMemcpyDeviceToHost, st));
         LSP_HIP(hipStreamSynchronize(st));
-        host.resize(height);
         pool.parallel_for(height, [&](size_t i) { host[i] = ctx->p2.hash(&rows[i * w], w); });
     } else {
         LSP_HIP(launch_hash_rows(m, height, layers, ctx->rc29_dev, ctx->p2.L, st));
@@ -160,28 +162,24 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers) {
             return d2h_fr(ctx, layers + 2 * height - 2);
         }
         LSP_HIP(launch_merkle_levels(layers, height, top, ctx->rc29_dev, ctx->p2.L, &off, &len, st));
-        host.resize(len);
-        LSP_HIP(hipMemcpyAsync(host.data(), layers + off, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
+        host = (Fr*)ctx->hbuf("merkle_top", (2 * len - 1) * sizeof(Fr));
+        LSP_HIP(hipMemcpyAsync(host, layers + off, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
         LSP_HIP(hipStreamSynchronize(st));
     }
-    const size_t first = host.size();  // the part already on the device (unless hashed here)
-    size_t lo = 0, n = first;
-    host.reserve(2 * first - 1);
+    const size_t first = len;  // the part already on the device (unless hashed here)
+    size_t lo = 0, n = first, end = first;
     while (n > 1) {
-        const size_t base = host.size();
-        host.resize(base + n / 2);
-        Fr* out = host.data() + base;
-        const Fr* in = host.data() + lo;
+        Fr* out = host + end;
+        const Fr* in = host + lo;
         pool.parallel_for(n / 2, [&](size_t i) { out[i] = ctx->p2.compress(in[2 * i], in[2 * i + 1]); });
-        lo = base;
+        lo = end;
+        end += n / 2;
         n /= 2;
     }
     const size_t skip = leaves_on_host ? 0 : first;  // host-made digests start here
-    if (host.size() > skip)
-        LSP_HIP(hipMemcpyAsync(layers + off + skip, host.data() + skip, (host.size() - skip) * sizeof(Fr),
-                               hipMemcpyHostToDevice, st));
-    LSP_HIP(hipStreamSynchronize(st));  // `host` must outlive the copy
-    return host.back();
+    if (end > skip)
+        LSP_HIP(hipMemcpyAsync(layers + off + skip, host + skip, (end - skip) * sizeof(Fr), hipMemcpyHostToDevice, st));
+    return host[end - 1];
 }
 
 static MatList one_mat(const Fr* p, uint32_t w) {

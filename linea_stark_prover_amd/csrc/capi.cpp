@@ -720,7 +720,8 @@ int lsp_prove_sharded(lsp_ctx* ctx, const lsp_fr* trace, size_t h, size_t w, con
 int lsp_proof_serialize(const lsp_proof* p, uint8_t* buf, size_t cap, size_t* len) {
     return guarded(nullptr, [&] {
         LSP_REQUIRE(p && len, LSP_E_ARG, "null");
-        const std::vector<uint8_t> b = serialize(*p);
+        if (p->wire.empty()) p->wire = serialize(*p);  // a size query and the copy serialize once
+        const std::vector<uint8_t>& b = p->wire;
         *len = b.size();
         if (buf) {
             LSP_REQUIRE(cap >= b.size(), LSP_E_ARG, "buffer too small");

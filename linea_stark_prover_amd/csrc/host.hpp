@@ -146,6 +146,7 @@ struct lsp_proof {
     lsp::Fr troot, qroot, pow_w;
     std::vector<lsp::Fr> tl, tn, qc, roots, final_poly;
     std::vector<lsp::lsp_query> queries;
+    mutable std::vector<uint8_t> wire;  // serialize() result, cached by lsp_proof_serialize
 };
 
 // a parsed CBOR RawPermutationTrace / RawLookupTrace (cbor.cpp)

@@ -675,44 +675,61 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
 }
 
 // --------------------------------------------------------- serialization
-static void put_u32(std::vector<uint8_t>& b, uint32_t x) {
-    for (int i = 0; i < 4; ++i) b.push_back((uint8_t)(x >> (8 * i)));
-}
-static void put_fr(std::vector<uint8_t>& b, const Fr& x) {
-    const Fr c = fr_to_canonical(x);
-    for (int i = 0; i < 8; ++i) put_u32(b, c.v[i]);
-}
+// little-endian words and canonical field elements, written in one pass into a
+// buffer sized up front
+namespace {
+struct Writer {
+    uint8_t* p;
+    void u32(uint32_t x) {
+        for (int i = 0; i < 4; ++i) *p++ = (uint8_t)(x >> (8 * i));
+    }
+    void fr(const Fr& x) {
+        const Fr c = fr_to_canonical(x);
+        for (int i = 0; i < 8; ++i) u32(c.v[i]);
+    }
+    void frs(const std::vector<Fr>& v) {
+        for (auto& x : v) fr(x);
+    }
+};
+}  // namespace
 
 std::vector<uint8_t> serialize(const lsp_proof& p) {
-    std::vector<uint8_t> b;
-    const char* magic = "LSPPRF01";
-    b.insert(b.end(), magic, magic + 8);
-    put_u32(b, p.log_h);
-    put_u32(b, p.log_q);
-    put_u32(b, p.w);
-    put_u32(b, (uint32_t)p.queries.size());
-    put_u32(b, (uint32_t)p.roots.size());
-    put_fr(b, p.troot);
-    put_fr(b, p.qroot);
-    for (auto& x : p.tl) put_fr(b, x);
-    for (auto& x : p.tn) put_fr(b, x);
-    for (auto& x : p.qc) put_fr(b, x);
-    for (auto& x : p.roots) put_fr(b, x);
-    for (auto& x : p.final_poly) put_fr(b, x);
-    put_fr(b, p.pow_w);
+    size_t nfr = 3 + p.tl.size() + p.tn.size() + p.qc.size() + p.roots.size() + p.final_poly.size(), nu32 = 5;
     for (auto& q : p.queries) {
-        for (auto& x : q.trow) put_fr(b, x);
-        put_u32(b, (uint32_t)q.tpath.size());
-        for (auto& x : q.tpath) put_fr(b, x);
-        for (auto& x : q.qrow) put_fr(b, x);
-        put_u32(b, (uint32_t)q.qpath.size());
-        for (auto& x : q.qpath) put_fr(b, x);
+        nfr += q.trow.size() + q.tpath.size() + q.qrow.size() + q.qpath.size() + q.sib.size();
+        for (auto& f : q.fpath) nfr += f.size();
+        nu32 += 2 + q.sib.size();
+    }
+    std::vector<uint8_t> b(8 + 4 * nu32 + 32 * nfr);
+    std::memcpy(b.data(), "LSPPRF01", 8);
+    Writer w{b.data() + 8};
+    w.u32(p.log_h);
+    w.u32(p.log_q);
+    w.u32(p.w);
+    w.u32((uint32_t)p.queries.size());
+    w.u32((uint32_t)p.roots.size());
+    w.fr(p.troot);
+    w.fr(p.qroot);
+    w.frs(p.tl);
+    w.frs(p.tn);
+    w.frs(p.qc);
+    w.frs(p.roots);
+    w.frs(p.final_poly);
+    w.fr(p.pow_w);
+    for (auto& q : p.queries) {
+        w.frs(q.trow);
+        w.u32((uint32_t)q.tpath.size());
+        w.frs(q.tpath);
+        w.frs(q.qrow);
+        w.u32((uint32_t)q.qpath.size());
+        w.frs(q.qpath);
         for (size_t r = 0; r < q.sib.size(); ++r) {
-            put_fr(b, q.sib[r]);
-            put_u32(b, (uint32_t)q.fpath[r].size());
-            for (auto& x : q.fpath[r]) put_fr(b, x);
+            w.fr(q.sib[r]);
+            w.u32((uint32_t)q.fpath[r].size());
+            w.frs(q.fpath[r]);
         }
     }
+    if (w.p != b.data() + b.size()) throw LspError(LSP_E_STATE, "proof serialization size mismatch");
     return b;
 }
 

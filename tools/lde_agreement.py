@@ -2,17 +2,22 @@
 rocprofv3 kernel trace of the same LDE (tools/pmc_round.sh 'kt' pass over
 tools/lde_probe.py, 3 calls): per-call sum of the LDE kernels.
 
-    python tools/lde_agreement.py profiles/r01g_lde_kernel_stats.csv profiles/r01g_bench.json [calls]
+    python tools/lde_agreement.py <kernel_stats.csv> <bench.json> [calls] [logcw]
 """
 import csv, json, sys
 
 stats, bench = sys.argv[1], sys.argv[2]
 calls = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 rows = list(csv.DictReader(open(stats)))
+# the trace LDE (w = 8) runs the LOGCW = 3 instantiations; the quotient LDE (w = 4) the LOGCW = 2 ones
+logcw = int(sys.argv[4]) if len(sys.argv) > 4 else 3
 lines, tot = [], 0.0
 for r in rows:
     name = r["Name"].replace("lsp::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
-    if "k_ntt_rm" in name or "k_pow_tables" in name:
+    targs = name[name.find("<") + 1:-1].split(", ") if "<" in name else []
+    # k_ntt_rm<DIF, MODE, LOGCW> (older traces: k_ntt_rm<DIF, MODE>)
+    ntt = "k_ntt_rm" in name and (len(targs) == 2 or targs[-1] == str(logcw))
+    if ntt or "k_pow_tables" in name:
         ms = float(r["TotalDurationNs"]) / calls / 1e6
         tot += ms
         lines.append(f"  {name:28s} calls {int(r['Calls']):3d}  avg {float(r['AverageNs']) / 1e3:9.1f} us  per LDE call {ms:7.3f} ms")

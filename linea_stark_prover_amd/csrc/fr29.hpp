@@ -154,6 +154,42 @@ __device__ __forceinline__ F29 f29_reduce(const F29& a) {
     return o;
 }
 
+__device__ __forceinline__ F29 f29_zero() {
+    F29 z;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) z.l[i] = 0;
+    return z;
+}
+
+// limb-wise sums without carry propagation (callers bound the limbs)
+__device__ __forceinline__ F29 f29_lazy2(const F29& a, const F29& b) {
+    F29 o;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o.l[i] = a.l[i] + b.l[i];
+    return o;
+}
+
+__device__ __forceinline__ F29 f29_lazy3(const F29& a, const F29& b, const F29& c) {
+    F29 o;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o.l[i] = a.l[i] + b.l[i] + c.l[i];
+    return o;
+}
+
+// a + 16 r - b, limb-wise without carries: 16 r is held with every low limb in
+// [2^29, 2^30) (borrowed from the limb above), so each difference is >= 0 for
+// normalised b with value < 16 r.  Limbs < 1.5 2^30: valid as one operand of a
+// product whose other operand is normalised (column sums < 2^63.5).
+__device__ __forceinline__ F29 f29_sub16(const F29& a, const F29& b) {
+    // 16 r (tools/gen_fr29mul.py --bound prints the derivation's check)
+    constexpr uint32_t L[9] = {0x20000010u, 0x28bfffffu, 0x20000427u, 0x2edfd9ffu, 0x300159a9u,
+                               0x28f2e1bcu, 0x35982d12u, 0x3d345949u, 0x12ab654u};
+    F29 o;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o.l[i] = a.l[i] + L[i] - b.l[i];
+    return o;
+}
+
 // x < 2^256 as 8 x 32-bit words -> 9 x 29-bit limbs (same integer)
 __device__ __forceinline__ F29 f29_repack_in(const Fr& x) {
     F29 o;

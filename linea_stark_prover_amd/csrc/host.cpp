@@ -316,7 +316,7 @@ lsp::HostPool& lsp_ctx::host_pool() {
     return *pool_;
 }
 
-const lsp::Fr* lsp_ctx::twiddle(uint32_t logH, bool inverse) {
+const lsp::Fr* lsp_ctx::twiddle29(uint32_t logH, bool inverse) {
     using namespace lsp;
     auto key = std::make_pair(logH, inverse ? 1 : 0);
     auto it = twiddles.find(key);
@@ -333,6 +333,7 @@ const lsp::Fr* lsp_ctx::twiddle(uint32_t logH, bool inverse) {
     Fr* out = nullptr;
     LSP_HIP(hipMalloc(&out, half * sizeof(Fr)));
     LSP_HIP(launch_powers(tab, L1, half, out, stream));
+    LSP_HIP(launch_to_f29form(out, out, half, stream));
     LSP_HIP(hipStreamSynchronize(stream));
     twiddles[key] = out;
     return out;

@@ -226,7 +226,8 @@ struct lsp_ctx {
     lsp::Fr* fbuf(const std::string& name, size_t n) { return (lsp::Fr*)buf(name, n * sizeof(lsp::Fr)); }
     // pinned host memory; growing it first drains the stream (a copy may still read it)
     void* hbuf(const std::string& name, size_t bytes);
-    const lsp::Fr* twiddle(uint32_t logH, bool inverse);
+    // w_H^x (or its inverse) for x < H/2, in the 29-bit Montgomery form the NTT multiplies by (k_ntt.hip)
+    const lsp::Fr* twiddle29(uint32_t logH, bool inverse);
     lsp::HostPool& host_pool();
     void sync();
 };

@@ -10,11 +10,21 @@
 //             i of column c by s_{k,c}^i / h on load (the coset twist), the
 //             last pass leaves the block in bit-reversed order -- exactly
 //             rows k*h + u = p_c(s_{k,c} w_h^bitrev(u)), the bit-reversed LDE.
-// A pass fuses k <= 8 radix-2 stages in LDS on a tile of 2^k positions x G
+// A pass fuses k <= 7 radix-2 stages in LDS on a tile of 2^k positions x G
 // adjacent groups x CW adjacent columns (CW*G = 8: every global access is a
-// 256-byte run of a row, or of adjacent rows).  Fr is 32 bytes; a tile is at
-// most 2048 elements = 64 KiB of the CU's 160 KiB LDS.  Butterflies whose
-// twiddle is 1 (DIT stage 0, DIF last stage) skip the product.
+// 256-byte run of a row, or of adjacent rows).  Butterflies whose twiddle is 1
+// (DIT stage 0, DIF last stage) skip the product.
+//
+// Arithmetic: the 29-bit-limb Montgomery product (fr29.hpp, R' = 2^261) on
+// ark-form elements.  An element X = x 2^256 is repacked bit for bit into 29-bit
+// limbs; twiddles and twist factors are stored in the 29-bit Montgomery form
+// W = w 2^261 (fr_to_f29form); the product X W 2^-261 = x w 2^256 is the ark
+// form of x w -- no conversion product anywhere.  Inside a pass the tile lives
+// in LDS in limb form (36 B per element), lazily reduced: every stored value is
+// normalised and < 8.3 r (sums reduced to < 2r, products < 8.06 r); a - b is
+// formed carry-free as a + 16r - b (f29_sub16).  Between passes the arrays hold
+// ark words reduced to < 2r; only the last forward pass writes canonical words.
+#include "fr29.hpp"
 #include "k_common.hpp"
 #include "kernels.hpp"
 
@@ -32,15 +42,29 @@ struct NttPass {
     uint32_t twist_per_col;  // 1: table index k*w + c, 0: table index k
     uint32_t logH, s0, k, logL, logG, w;
     uint32_t nchunk;    // column chunks of 2^LOGCW per row
+    uint32_t canon;     // 1: write canonical words (the transform's last pass)
     uint64_t narr;      // arrays (cosets) in dst
 };
+
+// x^i from a two-level table of 29-bit-form factors: the product of two
+// 29-bit-form values is the 29-bit form of the product
+__device__ __forceinline__ F29 pow2l29(const Fr* tab, uint32_t L1, uint64_t i) {
+    const F29 lo = f29_repack_in(tab[i & ((1ull << L1) - 1)]);
+    const F29 hi = f29_repack_in(tab[(1ull << L1) + (i >> L1)]);
+    return f29_mul(lo, hi);
+}
+
+__device__ __forceinline__ Fr f29_store(const F29& v, bool canon) {
+    const Fr o = f29_repack_out(f29_reduce(v));  // < 2r
+    return canon ? fr_reduce_once(o) : o;
+}
 
 // One tile: 2^k positions x 2^logG groups x 2^LOGCW columns (power-of-two
 // chunk, so every index below is shifts and masks; rows are 32-bit within
 // an array, H <= 2^31).
 template <bool DIF, int MODE, int LOGCW>
 __global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
-    extern __shared__ Fr lds[];
+    extern __shared__ F29 lds[];
     constexpr uint32_t CW = 1u << LOGCW;
     const uint32_t K = 1u << p.k, logG = p.logG, G = 1u << logG;
     const uint32_t logL = p.logL, Lmask = (1u << logL) - 1, rowshift = logL + p.k;
@@ -71,8 +95,8 @@ __global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
             g = tg & (G - 1);
         }
     };
-    // ---- twist factors s^row / h, once per row when every column shares the shift
-    Fr* fac = lds + n_el;  // K * G extra entries (launcher sizes the LDS for it)
+    // ---- twist factors s^row / h (29-bit form), once per row when every column shares the shift
+    F29* fac = lds + n_el;  // K * G extra entries (launcher sizes the LDS for it)
     const bool row_twist = MODE == PASS_FWD_FIRST && !p.twist_per_col;
     if (row_twist) {
         const Fr* tab = p.twist + (size_t)arr * ((1ull << p.L1) + (1ull << p.L2));
@@ -85,7 +109,7 @@ __global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
                 t = rg >> logG;
                 g = rg & (G - 1);
             }
-            fac[(t << logG) + g] = pow2l(tab, p.L1, row_of(t, g));
+            fac[(t << logG) + g] = pow2l29(tab, p.L1, row_of(t, g));
         }
         __syncthreads();
     }
@@ -95,20 +119,20 @@ __global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
         split(e, t, g, c);
         if (c >= cw) continue;
         const uint32_t row = row_of(t, g);
-        Fr v;
+        F29 v;
         if (MODE == PASS_INV_FIRST) {
-            v = p.src[(size_t)brev_bits(row, p.logH) * p.w + c0 + c];
+            v = f29_repack_in(p.src[(size_t)brev_bits(row, p.logH) * p.w + c0 + c]);
         } else if (MODE == PASS_FWD_FIRST) {
-            Fr f;
+            F29 f;
             if (row_twist) {
                 f = fac[(t << logG) + g];
             } else {
                 const Fr* tab = p.twist + ((size_t)arr * p.w + c0 + c) * ((1ull << p.L1) + (1ull << p.L2));
-                f = pow2l(tab, p.L1, row);
+                f = pow2l29(tab, p.L1, row);
             }
-            v = fr_mul(p.src[(size_t)row * p.w + c0 + c], f);
+            v = f29_mul(f29_repack_in(p.src[(size_t)row * p.w + c0 + c]), f);  // < 8.3 r
         } else {
-            v = base[(size_t)row * p.w + c0 + c];
+            v = f29_repack_in(base[(size_t)row * p.w + c0 + c]);
         }
         lds[(((t << logG) + g) << LOGCW) + c] = v;
     }
@@ -130,31 +154,39 @@ __global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
             const uint32_t t0 = ((pp >> logd) << (logd + 1)) | (pp & dmask);
             const uint32_t t1 = t0 + (1u << logd);
             const uint32_t a0 = (((t0 << logG) + g) << LOGCW) + c, a1 = (((t1 << logG) + g) << LOGCW) + c;
-            const Fr a = lds[a0], b = lds[a1];
+            const F29 a = lds[a0], b = lds[a1];
             if (trivial) {
-                lds[a0] = fr_add(a, b);
-                lds[a1] = fr_sub(a, b);
+                lds[a0] = f29_reduce(f29_lazy2(a, b));
+                lds[a1] = f29_reduce(f29_sub16(a, b));
                 continue;
             }
-            const Fr wv = p.tw[(row_of(t0, g) & tmask) << tshift];
+            const F29 wv = f29_repack_in(p.tw[(row_of(t0, g) & tmask) << tshift]);
             if (DIF) {
-                lds[a0] = fr_add(a, b);
-                lds[a1] = fr_mul(fr_sub(a, b), wv);
+                lds[a0] = f29_reduce(f29_lazy2(a, b));
+                lds[a1] = f29_mul(f29_sub16(a, b), wv);
             } else {
-                const Fr bw = fr_mul(b, wv);
-                lds[a0] = fr_add(a, bw);
-                lds[a1] = fr_sub(a, bw);
+                const F29 bw = f29_mul(b, wv);
+                lds[a0] = f29_reduce(f29_lazy2(a, bw));
+                lds[a1] = f29_reduce(f29_sub16(a, bw));
             }
         }
         __syncthreads();
     }
     // ---- store
+    const bool canon = p.canon != 0;
     for (uint32_t e = threadIdx.x; e < n_el; e += blockDim.x) {
         uint32_t t, g, c;
         split(e, t, g, c);
         if (c >= cw) continue;
-        base[(size_t)row_of(t, g) * p.w + c0 + c] = lds[(((t << logG) + g) << LOGCW) + c];
+        base[(size_t)row_of(t, g) * p.w + c0 + c] = f29_store(lds[(((t << logG) + g) << LOGCW) + c], canon);
     }
+}
+
+// ark-form words -> the 29-bit Montgomery form x 2^261 mod r, canonical, packed
+// in 8 words (twiddle and twist tables of k_ntt_rm)
+__global__ __launch_bounds__(256) void k_to_f29form(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n) {
+    const size_t i = gtid();
+    if (i < n) out[i] = f29_store(f29_from_fr(in[i]), true);
 }
 
 __global__ __launch_bounds__(256) void k_pow_tables(const Fr* __restrict__ bases, size_t nbases, uint32_t L1,
@@ -201,10 +233,11 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
     const uint32_t CW = 1u << logCW;
     const uint32_t logGmax = 3 - logCW;
     const uint32_t nchunk = (uint32_t)((w + CW - 1) / CW);
-    // k <= log2(2048 / (CW * G)) with CW * G <= 8
-    const uint32_t kmax = 8;
+    // k <= 7: a tile of <= 1024 limb-form elements (36 KiB) plus the twist factors
+    const uint32_t kmax = 7;
     uint32_t ks[16], np;
-    auto run = [&](bool dif, uint32_t narr, const Fr* src, Fr* dst, const Fr* tw, int first_mode) -> hipError_t {
+    auto run = [&](bool dif, uint32_t narr, const Fr* src, Fr* dst, const Fr* tw, int first_mode,
+                   bool canon_last) -> hipError_t {
         plan_passes(logh, kmax, ks, np);
         uint32_t s0 = 0;
         for (uint32_t q = 0; q < np; ++q) {
@@ -225,10 +258,11 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
             p.logG = logG;
             p.w = (uint32_t)w;
             p.nchunk = nchunk;
+            p.canon = (canon_last && q + 1 == np) ? 1u : 0u;
             p.narr = narr;
             const uint64_t tiles = (uint64_t)narr * ((1ull << logh) >> (k + logG)) * nchunk;
             // tile, plus one twist factor per row in the first forward pass
-            const size_t lds = ((size_t(1) << (k + logG)) * CW + (size_t(1) << (k + logG))) * sizeof(Fr);
+            const size_t lds = ((size_t(1) << (k + logG)) * CW + (size_t(1) << (k + logG))) * sizeof(F29);
             const int mode = q == 0 ? first_mode : PASS_INPLACE;
             const dim3 grid((unsigned)tiles), blk(256);
 #define LSP_NTT_LAUNCH(DIFV, MODEV)                                                                   \
@@ -268,9 +302,15 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
         }
         return hipSuccess;
     }
-    hipError_t e = run(false, 1, in, X, tw_inv, PASS_INV_FIRST);
+    hipError_t e = run(false, 1, in, X, tw_inv, PASS_INV_FIRST, false);
     if (e != hipSuccess) return e;
-    return run(true, ncosets, X, out, tw_fwd, PASS_FWD_FIRST);
+    return run(true, ncosets, X, out, tw_fwd, PASS_FWD_FIRST, true);
+}
+
+hipError_t launch_to_f29form(const Fr* in, Fr* out, size_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_to_f29form, dim3(nblocks(n, 256)), dim3(256), 0, st, in, out, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_pow_tables(const Fr* bases, size_t nbases, uint32_t L1, uint32_t L2, const Fr* scale, Fr* tabs,

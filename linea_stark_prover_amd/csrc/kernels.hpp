@@ -14,12 +14,16 @@ namespace lsp {
 // ------------------------------------------------------------ k_ntt.hip
 // Coset evaluations of the h x w row-major matrix `in`: `ncosets` blocks of h
 // rows (block k on the coset of twist table k), each in bit-reversed order,
-// into row-major `out`, via X (h x w scratch, left holding h * coefficients).  tw_inv / tw_fwd: w_h^-x / w_h^x,
-// x < h/2.  twist: two-level tables (L1, L2) of base s and scale 1/h, one per
-// coset (twist_per_col = 0) or per (coset, column) at index k*w + c.
+// into row-major `out` (canonical), via X (h x w scratch, left holding
+// h * coefficients reduced below 2r).  tw_inv / tw_fwd: w_h^-x / w_h^x, x < h/2;
+// twist: two-level tables (L1, L2) of base s and scale 1/h, one per coset
+// (twist_per_col = 0) or per (coset, column) at index k*w + c -- all tables in
+// the 29-bit Montgomery form (launch_to_f29form; k_ntt.hip).
 hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t ncosets, const Fr* tw_inv,
                       const Fr* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
                       hipStream_t st);
+// ark-form words -> the 29-bit Montgomery form (x 2^261 mod r), canonical, in place allowed
+hipError_t launch_to_f29form(const Fr* in, Fr* out, size_t n, hipStream_t st);
 // Two-level power tables: for each base b,
 // tab[b] = {b^j, j < 2^L1} ++ {b^(j 2^L1) * scale[b], j < 2^L2}   (scale nullable)
 hipError_t launch_pow_tables(const Fr* bases, size_t nbases, uint32_t L1, uint32_t L2, const Fr* scale,

@@ -27,28 +27,6 @@ __device__ __forceinline__ F29 sbox29(const F29& x) {
     return f29_mul(f29_sqr(x8), x);  // x^17
 }
 
-__device__ __forceinline__ F29 f29_zero() {
-    F29 z;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) z.l[i] = 0;
-    return z;
-}
-
-// limb-wise sums without carry propagation (see the bounds above)
-__device__ __forceinline__ F29 f29_lazy2(const F29& a, const F29& b) {
-    F29 o;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) o.l[i] = a.l[i] + b.l[i];
-    return o;
-}
-
-__device__ __forceinline__ F29 f29_lazy3(const F29& a, const F29& b, const F29& c) {
-    F29 o;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) o.l[i] = a.l[i] + b.l[i] + c.l[i];
-    return o;
-}
-
 // rc29: round constants in F29 form, new_from_rng order (initial external
 // [rf/2][3], terminal external [rf/2][3], internal [rp])
 template <uint32_t D>

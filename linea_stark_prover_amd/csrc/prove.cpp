@@ -124,7 +124,8 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
     const size_t per = (1ull << L1) + (1ull << L2);
     Fr* tabs = ctx->fbuf("lde_tabs", per * bases.size());
     LSP_HIP(launch_pow_tables(dbases, bases.size(), L1, L2, dbases + bases.size(), tabs, st));
-    LSP_HIP(launch_lde(d_in, X, d_out, w, logh, nk, ctx->twiddle(logh, true), ctx->twiddle(logh, false), tabs, L1,
+    LSP_HIP(launch_to_f29form(tabs, tabs, per * bases.size(), st));  // the NTT multiplies by 29-bit-form factors
+    LSP_HIP(launch_lde(d_in, X, d_out, w, logh, nk, ctx->twiddle29(logh, true), ctx->twiddle29(logh, false), tabs, L1,
                        L2, shared ? 0 : 1, st));
     // host vectors (bases, scales) must outlive the async copies
     LSP_HIP(hipStreamSynchronize(st));

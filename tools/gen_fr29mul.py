@@ -108,10 +108,38 @@ def bound():
     return worst
 
 
+def sub16_limbs():
+    """16 r with every low limb in [2^29, 2^30) (fr29.hpp f29_sub16)"""
+    r = sum(p << (29 * i) for i, p in enumerate(P29))
+    m = (1 << 29) - 1
+    c = [(16 * r >> (29 * i)) & m for i in range(8)] + [16 * r >> (29 * 8)]
+    limbs = [c[0] + (1 << 29)] + [c[i] + (1 << 29) - 1 for i in range(1, 8)] + [c[8] - 1]
+    assert sum(v << (29 * i) for i, v in enumerate(limbs)) == 16 * r
+    return limbs
+
+
+def bound_sub16():
+    """worst column sum of (a + 16r - b) * w, a normalised, w canonical"""
+    r = sum(p << (29 * i) for i, p in enumerate(P29))
+    L = sub16_limbs()
+    a = [(1 << 29) - 1 + L[i] for i in range(8)] + [(24 * r) >> 232]
+    b = [(1 << 29) - 1] * 8 + [r >> 232]
+    m, worst, carry = (1 << 32) - 1, 0, 0
+    for k in range(17):
+        tot = sum(a[j] * b[k - j] for j in range(9) if 0 <= k - j <= 8)
+        tot += sum(m * P29[k - j] for j in range(9) if 1 <= k - j <= 8) + carry + (m if k < 9 else 0)
+        worst, carry = max(worst, tot), tot >> 29
+    return worst
+
+
 def main():
     if "--bound" in sys.argv:
         w = bound()
         print("worst column sum < 2^%.3f" % math.log2(w))
+        assert w < 1 << 64
+        print("f29_sub16 limbs:", ", ".join(hex(v) for v in sub16_limbs()))
+        w = bound_sub16()
+        print("worst column sum, (a + 16r - b) * w: < 2^%.3f" % math.log2(w))
         assert w < 1 << 64
         return
     chains = int(sys.argv[1]) if len(sys.argv) > 1 else 1

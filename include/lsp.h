@@ -170,6 +170,23 @@ int lsp_quotient_values(lsp_ctx *ctx, const lsp_fr *lde, size_t h, size_t w, con
  * LDE (the low coset shift*H_h) at z: ys_out gets w values (host memory). */
 int lsp_interpolate_coset(lsp_ctx *ctx, const lsp_fr *lde_bitrev, size_t h, size_t w, const lsp_fr *shift,
                           const lsp_fr *z, lsp_fr *ys_out, int mem);
+/* compute_inverse_denominators of TwoAdicFriPcs::open [EXT p3-fri], reached
+ * from p3_uni_stark::prove (bin/src/main.rs:80-86) through pcs.open:
+ * out[p*N + i] = 1 / (points[p] - shift * w_N^bitrev(i)), N = 2^log_n, i.e.
+ * against the bit-reversed LDE domain shift*H_N (shift = GENERATOR there).
+ * Every point must lie outside that coset.  out: npoints * N elements. */
+int lsp_inverse_denominators(lsp_ctx *ctx, const lsp_fr *points, size_t npoints, uint32_t log_n,
+                             const lsp_fr *shift, lsp_fr *out, int mem);
+/* The "reduce rows" step of TwoAdicFriPcs::open [EXT p3-fri] for one matrix
+ * (n rows of width w, bit-reversed LDE) opened at npoints points:
+ *   for each point p: ro[i] += off * (sum_c alpha^c ys[p][c] - sum_c alpha^c M[i][c]) * inv_denoms[p*n + i];
+ *                     off *= alpha^w
+ * ys: npoints x w (host memory); alpha_pow_offset (host, in/out) is the running
+ * alpha^{num_reduced} of this log-height, advanced as Plonky3 advances it, so
+ * successive calls over the opened matrices in commit order build the FRI
+ * input vector ro (n elements, in/out). */
+int lsp_open_reduce(lsp_ctx *ctx, const lsp_fr *mat, size_t n, size_t w, const lsp_fr *inv_denoms, const lsp_fr *ys,
+                    size_t npoints, const lsp_fr *alpha, lsp_fr *alpha_pow_offset, lsp_fr *ro, int mem);
 /* p3-field batch_multiplicative_inverse */
 int lsp_batch_inverse(lsp_ctx *ctx, const lsp_fr *in, size_t n, lsp_fr *out, int mem);
 

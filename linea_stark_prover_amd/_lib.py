@@ -84,6 +84,10 @@ _SIGS = {
                                            c_fr_p, ctypes.c_int]),
     "lsp_interpolate_coset": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, c_fr_p,
                                              c_fr_p, c_fr_p, ctypes.c_int]),
+    "lsp_inverse_denominators": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_uint32, c_fr_p,
+                                                c_fr_p, ctypes.c_int]),
+    "lsp_open_reduce": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, c_fr_p, c_fr_p,
+                                       ctypes.c_size_t, c_fr_p, c_fr_p, c_fr_p, ctypes.c_int]),
     "lsp_batch_inverse": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, c_fr_p, ctypes.c_int]),
     "lsp_prove": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
                                  ctypes.c_size_t, c_fr_p, ctypes.c_size_t, ctypes.c_int,

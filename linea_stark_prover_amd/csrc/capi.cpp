@@ -529,6 +529,66 @@ int lsp_batch_inverse(lsp_ctx* ctx, const lsp_fr* in, size_t n, lsp_fr* out, int
     });
 }
 
+int lsp_inverse_denominators(lsp_ctx* ctx, const lsp_fr* points, size_t npoints, uint32_t log_n, const lsp_fr* shift,
+                             lsp_fr* out, int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && points && shift && npoints >= 1, LSP_E_ARG, "bad inverse_denominators arguments");
+        LSP_REQUIRE(log_n <= 40, LSP_E_SIZE, "log_n too large");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const size_t N = (size_t)1 << log_n;
+        Fr* dout = dev_out(ctx, out, npoints * N, mem, "api_out");
+        uint32_t L1 = (log_n + 1) / 2, L2 = log_n - L1;
+        Fr* tab = ctx->fbuf("api_tab", (1ull << L1) + (1ull << L2));
+        Fr* b = ctx->fbuf("api_tab_base", 1);
+        const Fr gN = host_two_adic_generator(log_n);
+        LSP_HIP(hipMemcpyAsync(b, &gN, sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+        LSP_HIP(launch_pow_tables(b, 1, L1, L2, nullptr, tab, ctx->stream));
+        Fr* den = ctx->fbuf("o_den", npoints * N);
+        for (size_t p = 0; p < npoints; ++p)
+            LSP_HIP(launch_open_denoms(to_fr(points[p]), to_fr(*shift), tab, L1, log_n, N, den + p * N,
+                                       ctx->stream));
+        LSP_HIP(launch_batch_inverse(den, dout, npoints * N, ctx->stream));
+        finish_out(ctx, out, dout, npoints * N, mem);
+    });
+}
+
+int lsp_open_reduce(lsp_ctx* ctx, const lsp_fr* mat, size_t n, size_t w, const lsp_fr* inv_denoms, const lsp_fr* ys,
+                    size_t npoints, const lsp_fr* alpha, lsp_fr* alpha_pow_offset, lsp_fr* ro, int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && ys && alpha && alpha_pow_offset && ro && npoints >= 1 && w >= 1 && n >= 1, LSP_E_ARG,
+                    "bad open_reduce arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const Fr* dm = dev_in(ctx, mat, n * w, mem, "api_in");
+        const Fr* dinv = dev_in(ctx, inv_denoms, npoints * n, mem, "api_in2");
+        Fr* dro = const_cast<Fr*>(dev_in(ctx, ro, n, mem, "api_out"));
+        // host side: alpha^c (c < w), per point the offset and offset * sum_c alpha^c y_c
+        const Fr A = to_fr(*alpha);
+        std::vector<Fr> apw(w), coef(2 * npoints);
+        Fr pw = fr_one();
+        for (size_t c = 0; c < w; ++c) {
+            apw[c] = pw;
+            pw = fr_mul(pw, A);
+        }
+        Fr off = to_fr(*alpha_pow_offset);
+        for (size_t p = 0; p < npoints; ++p) {
+            Fr ry = fr_zero();
+            for (size_t c = 0; c < w; ++c) ry = fr_add(ry, fr_mul(apw[c], to_fr(ys[p * w + c])));
+            coef[p] = off;
+            coef[npoints + p] = fr_mul(off, ry);
+            off = fr_mul(off, pw);  // pw = alpha^w: the offset advances by the matrix width
+        }
+        Fr* dc = ctx->fbuf("api_coef", w + 2 * npoints);
+        LSP_HIP(hipMemcpyAsync(dc, apw.data(), w * sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+        LSP_HIP(hipMemcpyAsync(dc + w, coef.data(), 2 * npoints * sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+        LSP_HIP(launch_reduce_matrix(dm, n, (uint32_t)w, dc, (uint32_t)npoints, dinv, dc + w, dc + w + npoints, dro,
+                                     ctx->stream));
+        finish_out(ctx, ro, dro, n, mem);
+        *alpha_pow_offset = from_fr(off);
+    });
+}
+
 int lsp_prove(lsp_ctx* ctx, const lsp_fr* trace, size_t h, size_t w, const int32_t* air, size_t air_len,
               const lsp_fr* pubv, size_t npub, int mem, lsp_proof** out) {
     return guarded(ctx, [&] {

@@ -80,6 +80,22 @@ __global__ __launch_bounds__(256) void k_reduce_rows(ReduceArgs a) {
     a.out[i] = acc;
 }
 
+// coef[0..npts) = alpha offsets, coef[npts..2 npts) = offset * reduced ys; apw = alpha^c, c < w
+__global__ __launch_bounds__(256) void k_reduce_matrix(const Fr* __restrict__ M, size_t n, uint32_t w,
+                                                       const Fr* __restrict__ apw, uint32_t npts,
+                                                       const Fr* __restrict__ inv, const Fr* __restrict__ off,
+                                                       const Fr* __restrict__ offys, Fr* __restrict__ ro) {
+    const size_t i = gtid();
+    if (i >= n) return;
+    const Fr* row = M + i * w;
+    Fr rr = fr_zero();
+    for (uint32_t c = 0; c < w; ++c) rr = fr_add(rr, fr_mul(apw[c], row[c]));
+    Fr acc = ro[i];
+    for (uint32_t p = 0; p < npts; ++p)
+        acc = fr_add(acc, fr_mul(fr_sub(offys[p], fr_mul(off[p], rr)), inv[(size_t)p * n + i]));
+    ro[i] = acc;
+}
+
 __global__ __launch_bounds__(256) void k_fri_fold(const Fr* __restrict__ v, size_t m, Fr half, Fr half_beta,
                                                   const Fr* __restrict__ tab, uint32_t L1, uint32_t logm,
                                                   uint64_t i0, Fr* __restrict__ out) {
@@ -112,6 +128,13 @@ hipError_t launch_sum_partials(const Fr* partial, uint32_t nb, uint32_t w, Fr* o
 
 hipError_t launch_reduce_rows(const ReduceArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_reduce_rows, dim3(nblocks(a.n, 256)), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_reduce_matrix(const Fr* M, size_t n, uint32_t w, const Fr* apw, uint32_t npts, const Fr* inv,
+                                const Fr* off, const Fr* offys, Fr* ro, hipStream_t st) {
+    hipLaunchKernelGGL(k_reduce_matrix, dim3(nblocks(n, 256)), dim3(256), 0, st, M, n, w, apw, npts, inv, off, offys,
+                       ro);
     return hipGetLastError();
 }
 

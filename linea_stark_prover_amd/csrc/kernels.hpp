@@ -143,6 +143,10 @@ struct ReduceArgs {
     size_t n;
 };
 hipError_t launch_reduce_rows(const ReduceArgs& a, hipStream_t st);
+// one matrix opened at npts points (the generic reduce of TwoAdicFriPcs::open):
+// ro[i] += sum_p (offys[p] - off[p] * sum_c apw[c] M[i][c]) * inv[p*n + i]
+hipError_t launch_reduce_matrix(const Fr* M, size_t n, uint32_t w, const Fr* apw, uint32_t npts, const Fr* inv,
+                                const Fr* off, const Fr* offys, Fr* ro, hipStream_t st);
 // FRI fold of v (2m values) -> out (m values); tab: two-level table of w_{2M}^-1
 // where M = 2^logm is the whole folded length (logm < 0: M = m) and v holds
 // the pairs from global pair index i0 on (a shard of the vector).

@@ -8,6 +8,8 @@ Reference item                                   -> here
   TwoAdicFriGenericConfig::fold_matrix/fold_row   -> TwoAdicFriGenericConfig
   p3_uni_stark::quotient_values                   -> Context.quotient_values
   p3_interpolation::interpolate_coset             -> Context.interpolate_coset
+  TwoAdicFriPcs::open compute_inverse_denominators -> Context.inverse_denominators
+  TwoAdicFriPcs::open reduce rows                 -> Context.open_reduce
   p3_uni_stark::prove / verify (main.rs:80-96)    -> prove / verify
 
 Arrays are numpy uint64 with a trailing axis of 4 limbs (Montgomery form).
@@ -176,6 +178,31 @@ class Context:
         self._chk(L.lib().lsp_interpolate_coset(self.h, _ptr(m), h, w, _ptr(sh), _ptr(zz), _ptr(out),
                                                 L.LSP_MEM_HOST))
         return out
+
+    def inverse_denominators(self, points, log_n: int, shift) -> np.ndarray:
+        """compute_inverse_denominators: (len(points), 2^log_n, 4) array of
+        1/(z - shift w_N^bitrev(i))."""
+        pts = _fr_arr(points).reshape(-1, 4)
+        sh = _fr_arr(shift).reshape(-1, 4)
+        out = np.zeros((pts.shape[0], 1 << log_n, 4), np.uint64)
+        self._chk(L.lib().lsp_inverse_denominators(self.h, _ptr(pts), pts.shape[0], log_n, _ptr(sh), _ptr(out),
+                                                   L.LSP_MEM_HOST))
+        return out
+
+    def open_reduce(self, mat: np.ndarray, inv_denoms: np.ndarray, ys: np.ndarray, alpha, alpha_pow_offset,
+                    ro: np.ndarray) -> np.ndarray:
+        """Reduce rows of one opened matrix (n x w) at len(ys) points into ro
+        (updated in place); returns the advanced alpha-power offset."""
+        m = _fr_arr(mat)
+        n, w = m.shape[0], m.shape[1]
+        inv = _fr_arr(inv_denoms).reshape(-1, n, 4)
+        y = _fr_arr(ys).reshape(inv.shape[0], w, 4)
+        al = _fr_arr(alpha).reshape(-1, 4)
+        off = _fr_arr(alpha_pow_offset).reshape(-1, 4).copy()
+        assert ro.dtype == np.uint64 and ro.shape == (n, 4) and ro.flags["C_CONTIGUOUS"]
+        self._chk(L.lib().lsp_open_reduce(self.h, _ptr(m), n, w, _ptr(inv), _ptr(y), inv.shape[0], _ptr(al),
+                                          _ptr(off), _ptr(ro), L.LSP_MEM_HOST))
+        return off[0]
 
     def batch_inverse(self, x: np.ndarray) -> np.ndarray:
         x = _fr_arr(x).reshape(-1, 4)

@@ -697,6 +697,32 @@ def interpolate_coset(low_rows_bitrev: List[List[int]], shift: int, z: int) -> L
     return [s * f % P for s in sums]
 
 
+def inverse_denominators(log_n: int, shift: int, points: Sequence[int]) -> List[List[int]]:
+    """compute_inverse_denominators of TwoAdicFriPcs::open [EXT p3-fri] (SURVEY 8(a) A12):
+    per point z, 1/(z - shift * w_N^bitrev(i)) over the bit-reversed coset (reached from
+    p3_uni_stark::prove, bin/src/main.rs:80-86)."""
+    N = 1 << log_n
+    g = two_adic_generator(log_n)
+    xs = reverse_slice_index_bits([shift * pow(g, i, P) % P for i in range(N)])
+    return [[inv(z - x) for x in xs] for z in points]
+
+
+def open_reduce(mat_rows, inv_denoms, ys, alpha: int, alpha_pow_offset: int, ro: List[int]) -> int:
+    """The reduce-rows step of TwoAdicFriPcs::open [EXT p3-fri] (SURVEY 8(a) A14) for one
+    matrix opened at len(ys) points: ro[i] += off * (sum_c alpha^c y_c - sum_c alpha^c M[i][c])
+    * inv[z][i], then off *= alpha^width.  Updates ro in place; returns the new offset."""
+    w = len(mat_rows[0])
+    apw = [pow(alpha, c, P) for c in range(w)]
+    rr = [sum(a * v for a, v in zip(apw, row)) % P for row in mat_rows]
+    off = alpha_pow_offset
+    for invz, yz in zip(inv_denoms, ys):
+        red_ys = sum(a * y for a, y in zip(apw, yz)) % P
+        for i in range(len(ro)):
+            ro[i] = (ro[i] + off * (red_ys - rr[i]) % P * invz[i]) % P
+        off = off * pow(alpha, w, P) % P
+    return off
+
+
 def fold_vector(v: List[int], beta: int) -> List[int]:
     """TwoAdicFriGenericConfig::fold_matrix over RowMajorMatrix(v, 2)."""
     m = len(v) // 2
@@ -779,9 +805,7 @@ def prove(cfgs, trace_rows: List[List[int]], pub: List[int], pp: Poseidon2Params
     log["alpha_fri"] = alpha_fri
     N = h << lb
     logN = log_h + lb
-    gN = two_adic_generator(logN)
-    xs = reverse_slice_index_bits([GENERATOR * pow(gN, i, P) % P for i in range(N)])
-    invd = {z: [inv(z - x) for x in xs] for z in (zeta, zeta_next)}
+    invd = dict(zip((zeta, zeta_next), inverse_denominators(logN, GENERATOR, [zeta, zeta_next])))
 
     low = lde[:h]
     ys_zeta = interpolate_coset(low, GENERATOR, zeta)
@@ -790,21 +814,10 @@ def prove(cfgs, trace_rows: List[List[int]], pub: List[int], pp: Poseidon2Params
     ys_q = interpolate_coset(qlow, GENERATOR, zeta)   # one value per chunk (width-1 matrices)
 
     ro = [0] * N
-    num_reduced = 0
-
-    def reduce(mat_rows, ys, z):
-        nonlocal num_reduced
-        apow = pow(alpha_fri, num_reduced, P)
-        red_ys = sum(pow(alpha_fri, c, P) * y for c, y in enumerate(ys)) % P
-        for i in range(N):
-            rr = sum(pow(alpha_fri, c, P) * v for c, v in enumerate(mat_rows[i])) % P
-            ro[i] = (ro[i] + apow * (red_ys - rr) % P * invd[z][i]) % P
-        num_reduced += len(ys)
-
-    reduce(lde, ys_zeta, zeta)
-    reduce(lde, ys_next, zeta_next)
+    off = 1  # alpha_fri^num_reduced
+    off = open_reduce(lde, [invd[zeta], invd[zeta_next]], [ys_zeta, ys_next], alpha_fri, off, ro)
     for j in range(q):
-        reduce([[r[j]] for r in q_lde], [ys_q[j]], zeta)
+        off = open_reduce([[r[j]] for r in q_lde], [invd[zeta]], [[ys_q[j]]], alpha_fri, off, ro)
     log["fri_input"] = list(ro)
 
     # ---- FRI commit phase

@@ -183,6 +183,39 @@ def test_interpolate_coset_matches_pyoracle(gpu_ctx):
     assert got == exp
 
 
+# ------------------------------------- open: inverse denominators, reduce
+@pytest.mark.parametrize("log_n", [0, 3, 7])
+def test_inverse_denominators_match_pyoracle(gpu_ctx, log_n):
+    from linea_stark_prover_amd.field import to_mont
+    rng = np.random.default_rng(100 + log_n)
+    pts = rand_fr(rng, (3,))
+    got = gpu_ctx.inverse_denominators(pts, log_n, to_mont([O.GENERATOR]))
+    exp = O.inverse_denominators(log_n, O.GENERATOR, ints(pts))
+    assert [ints(got[p]) for p in range(3)] == exp
+
+
+@pytest.mark.parametrize("n,w,npts", [(8, 3, 2), (64, 8, 2), (32, 1, 1), (1, 5, 3)])
+def test_open_reduce_matches_pyoracle(gpu_ctx, n, w, npts):
+    """two matrices reduced one after the other (the offset carries over), as
+    TwoAdicFriPcs::open reduces trace@(zeta, zeta_next) then the quotient chunks"""
+    from linea_stark_prover_amd.field import to_mont
+    rng = np.random.default_rng(n * 100 + w)
+    m1, m2 = rand_fr(rng, (n, w)), rand_fr(rng, (n, 2))
+    inv = rand_fr(rng, (npts, n))
+    y1, y2 = rand_fr(rng, (npts, w)), rand_fr(rng, (1, 2))
+    alpha = rand_fr(rng, (1,))
+    ro = rand_fr(rng, (n,))
+    ro_exp = ints(ro)
+    a = ints(alpha)[0]
+    off = gpu_ctx.open_reduce(m1, inv, y1, alpha, to_mont([1]), ro)
+    off = gpu_ctx.open_reduce(m2, inv[:1], y2, alpha, off, ro)
+    e = O.open_reduce([ints(m1[i]) for i in range(n)], [ints(inv[p]) for p in range(npts)],
+                      [ints(y1[p]) for p in range(npts)], a, 1, ro_exp)
+    e = O.open_reduce([ints(m2[i]) for i in range(n)], [ints(inv[0])], [ints(y2[0])], a, e, ro_exp)
+    assert ints(ro) == ro_exp
+    assert ints(off.reshape(1, 4))[0] == e == pow(a, npts * w + 2, P)
+
+
 # -------------------------------------------------------------- quotient
 def _perm_setup(logn, ncols, oracle_lib):
     s = O.setup_from_seed()

@@ -446,7 +446,7 @@ int lsp_quotient_values(lsp_ctx* ctx, const lsp_fr* lde, size_t h, size_t w, con
         Fr* den = ctx->fbuf("q_den", Q);
         Fr* inv_den = ctx->fbuf("q_invden", Q);
         LSP_HIP(launch_selector_denoms(tab, L1, GEN, wh_inv, Q, den, ctx->stream));
-        LSP_HIP(launch_batch_inverse(den, inv_den, Q, ctx->stream));
+        LSP_HIP(launch_batch_inverse(den, inv_den, Q, ctx->stream, ctx->bi_scratch(Q)));
         std::vector<Fr> zz(2 * q);
         const Fr gh = fr_pow_u64(GEN, h), gl = host_two_adic_generator(log_q);
         Fr gg = one;
@@ -501,7 +501,7 @@ int lsp_interpolate_coset(lsp_ctx* ctx, const lsp_fr* lde_bitrev, size_t h, size
         Fr* den = ctx->fbuf("o_den", h);
         Fr* inv = ctx->fbuf("o_invz", h);
         LSP_HIP(launch_open_denoms(Z, S, tab, L1, logh, h, den, ctx->stream));
-        LSP_HIP(launch_batch_inverse(den, inv, h, ctx->stream));
+        LSP_HIP(launch_batch_inverse(den, inv, h, ctx->stream, ctx->bi_scratch(h)));
         Fr* partial = ctx->fbuf("o_partial", ((h + 1023) / 1024) * w);
         Fr* sums = ctx->fbuf("o_sums", w);
         uint32_t nb = 0;
@@ -524,7 +524,7 @@ int lsp_batch_inverse(lsp_ctx* ctx, const lsp_fr* in, size_t n, lsp_fr* out, int
         const Fr* din = dev_in(ctx, in, n, mem, "api_in");
         Fr* dout = dev_out(ctx, out, n, mem, "api_out");
         LSP_REQUIRE(din != dout, LSP_E_ARG, "batch_inverse cannot run in place");
-        LSP_HIP(launch_batch_inverse(din, dout, n, ctx->stream));
+        LSP_HIP(launch_batch_inverse(din, dout, n, ctx->stream, ctx->bi_scratch(n)));
         finish_out(ctx, out, dout, n, mem);
     });
 }
@@ -548,7 +548,7 @@ int lsp_inverse_denominators(lsp_ctx* ctx, const lsp_fr* points, size_t npoints,
         for (size_t p = 0; p < npoints; ++p)
             LSP_HIP(launch_open_denoms(to_fr(points[p]), to_fr(*shift), tab, L1, log_n, N, den + p * N,
                                        ctx->stream));
-        LSP_HIP(launch_batch_inverse(den, dout, npoints * N, ctx->stream));
+        LSP_HIP(launch_batch_inverse(den, dout, npoints * N, ctx->stream, ctx->bi_scratch(npoints * N)));
         finish_out(ctx, out, dout, npoints * N, mem);
     });
 }

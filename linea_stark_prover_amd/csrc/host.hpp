@@ -224,6 +224,8 @@ struct lsp_ctx {
 
     void* buf(const std::string& name, size_t bytes);
     lsp::Fr* fbuf(const std::string& name, size_t n) { return (lsp::Fr*)buf(name, n * sizeof(lsp::Fr)); }
+    // scratch of a hierarchical batch inverse of n elements (launch_batch_inverse)
+    lsp::Fr* bi_scratch(size_t n) { return fbuf("bi_scratch", lsp::batch_inverse_scratch(n) + 1); }
     // pinned host memory; growing it first drains the stream (a copy may still read it)
     void* hbuf(const std::string& name, size_t bytes);
     // w_H^x (or its inverse) for x < H/2, in the 29-bit Montgomery form the NTT multiplies by (k_ntt.hip)

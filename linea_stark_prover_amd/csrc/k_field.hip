@@ -1,11 +1,116 @@
 // Batch inversion (p3-field batch_multiplicative_inverse) and the gather used
 // to pull query openings off the device in one copy.
+#include "fr29.hpp"
 #include "k_common.hpp"
 #include "kernels.hpp"
 
 namespace lsp {
 
 namespace {
+// Batch inversion, hierarchical (Montgomery's trick at every level):
+//   up    thread t owns elements t, t+T, t+2T, ... (`chunk` of them, interleaved
+//         so every pass is coalesced): out[i] = prefix product before i, and
+//         prod[t] = the chunk's product;
+//   the T chunk products are inverted the same way, recursively, down to a
+//   base of <= BI_BASE elements that one workgroup inverts with a product
+//   tree in LDS and ONE Fermat inverse (on the 29-bit multiplier);
+//   down  thread t walks its chunk backwards from 1/prod[t].
+// Cost ~3 products per element plus one inversion for the whole batch; the
+// critical path is a few short chains plus that one inversion.
+constexpr uint32_t BI_CHUNK = 16;
+constexpr uint32_t BI_THREADS = 256;
+constexpr uint32_t BI_BASE = BI_THREADS * 16;
+
+__global__ __launch_bounds__(256) void k_bi_up(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n, size_t T,
+                                               uint32_t chunk, Fr* __restrict__ prod) {
+    const size_t t = gtid();
+    if (t >= T) return;
+    Fr acc = fr_one();
+    for (uint32_t j = 0; j < chunk; ++j) {
+        const size_t i = t + (size_t)j * T;
+        if (i >= n) break;
+        out[i] = acc;
+        acc = fr_mul(acc, in[i]);
+    }
+    prod[t] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_bi_down(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n, size_t T,
+                                                 uint32_t chunk, const Fr* __restrict__ inv_prod) {
+    const size_t t = gtid();
+    if (t >= T) return;
+    Fr inv = inv_prod[t];
+    uint32_t cnt = 0;
+    while (cnt < chunk && t + (size_t)cnt * T < n) ++cnt;
+    for (uint32_t j = cnt; j-- > 0;) {
+        const size_t i = t + (size_t)j * T;
+        const Fr o = fr_mul(inv, out[i]);
+        inv = fr_mul(inv, in[i]);
+        out[i] = o;
+    }
+}
+
+// a^(r-2) on the 29-bit multiplier (Fermat; the inverse of zero is zero)
+__device__ Fr fr_inv_f29(const Fr& a) {
+    const F29 x = f29_from_fr(a);
+    F29 r = x;  // the exponent's top bit
+    for (int w = 7; w >= 0; --w) {
+        // r - 2: r[0] = 1, so the subtraction borrows from word 1
+        const uint32_t e = w == 0 ? 0xffffffffu : (w == 1 ? LSP_MOD1 - 1u : mod_word(w));
+        const int top = w == 7 ? 31 - __builtin_clz(e) - 1 : 31;
+        for (int k = top; k >= 0; --k) {
+            r = f29_sqr(r);
+            if ((e >> k) & 1u) r = f29_mul(r, x);
+        }
+    }
+    return f29_to_fr(r);
+}
+
+// n <= BI_BASE: per-thread chunks (stride BI_THREADS), a product tree over the
+// BI_THREADS chunk products in LDS, one inversion, back down the tree
+__global__ __launch_bounds__(BI_THREADS) void k_bi_base(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n) {
+    __shared__ Fr tree[2 * BI_THREADS];  // node k: children 2k, 2k+1; leaves at BI_THREADS + t
+    const uint32_t t = threadIdx.x;
+    Fr acc = fr_one();
+    for (size_t i = t; i < n; i += BI_THREADS) {
+        out[i] = acc;
+        acc = fr_mul(acc, in[i]);
+    }
+    tree[BI_THREADS + t] = acc;
+    __syncthreads();
+    for (uint32_t w = BI_THREADS / 2; w >= 1; w >>= 1) {
+        if (t < w) tree[w + t] = fr_mul(tree[2 * (w + t)], tree[2 * (w + t) + 1]);
+        __syncthreads();
+    }
+    if (t == 0) tree[1] = fr_inv_f29(tree[1]);
+    __syncthreads();
+    // top-down: node k holds 1/(product of its subtree); children swap products
+    for (uint32_t w = 1; w < BI_THREADS; w <<= 1) {
+        Fr l, r;
+        if (t < w) {
+            const Fr iv = tree[w + t];
+            l = fr_mul(iv, tree[2 * (w + t) + 1]);
+            r = fr_mul(iv, tree[2 * (w + t)]);
+        }
+        __syncthreads();
+        if (t < w) {
+            tree[2 * (w + t)] = l;
+            tree[2 * (w + t) + 1] = r;
+        }
+        __syncthreads();
+    }
+    Fr inv = tree[BI_THREADS + t];
+    if (t >= n) return;
+    const size_t last = t + ((n - 1 - t) / BI_THREADS) * BI_THREADS;
+    for (size_t i = last;; i -= BI_THREADS) {
+        const Fr o = fr_mul(inv, out[i]);
+        inv = fr_mul(inv, in[i]);
+        out[i] = o;
+        if (i < BI_THREADS) break;
+    }
+}
+
+// single-level kernel (no scratch): one Fermat inverse per thread
 // Thread t owns elements t, t+T, t+2T, ... (`chunk` of them, interleaved so every
 // pass is coalesced): a prefix product, one Fermat inverse, the back pass.  The
 // inverse (~380 products) is one instruction stream per wave whatever the
@@ -64,13 +169,38 @@ __global__ __launch_bounds__(256) void k_assemble_chunks(const Fr* __restrict__ 
 }
 }  // namespace
 
-hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st) {
+size_t batch_inverse_scratch(size_t n) {
+    size_t tot = 0;
+    while (n > BI_BASE) {
+        n = (n + BI_CHUNK - 1) / BI_CHUNK;
+        tot += 2 * n;
+    }
+    return tot;
+}
+
+hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st, Fr* scratch) {
     if (!n) return hipSuccess;
-    // lanes for one wave per SIMD (256 CUs x 4 SIMDs x 64), 8 .. 256 elements each
-    uint32_t chunk = 8;
-    while (chunk < 256 && (size_t)chunk * 65536 < n) chunk *= 2;
-    const size_t T = (n + chunk - 1) / chunk;
-    hipLaunchKernelGGL(k_batch_inverse, dim3(nblocks(T, 256)), dim3(256), 0, st, in, out, n, T, chunk);
+    if (!scratch && n > BI_BASE) {
+        // lanes for one wave per SIMD (256 CUs x 4 SIMDs x 64), 8 .. 256 elements each
+        uint32_t chunk = 8;
+        while (chunk < 256 && (size_t)chunk * 65536 < n) chunk *= 2;
+        const size_t T = (n + chunk - 1) / chunk;
+        hipLaunchKernelGGL(k_batch_inverse, dim3(nblocks(T, 256)), dim3(256), 0, st, in, out, n, T, chunk);
+        return hipGetLastError();
+    }
+    if (n <= BI_BASE) {
+        hipLaunchKernelGGL(k_bi_base, dim3(1), dim3(BI_THREADS), 0, st, in, out, n);
+        return hipGetLastError();
+    }
+    const size_t T = (n + BI_CHUNK - 1) / BI_CHUNK;
+    Fr* prod = scratch;
+    Fr* inv_prod = scratch + T;
+    hipLaunchKernelGGL(k_bi_up, dim3(nblocks(T, 256)), dim3(256), 0, st, in, out, n, T, BI_CHUNK, prod);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = launch_batch_inverse(prod, inv_prod, T, st, scratch + 2 * T);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_bi_down, dim3(nblocks(T, 256)), dim3(256), 0, st, in, out, n, T, BI_CHUNK, inv_prod);
     return hipGetLastError();
 }
 

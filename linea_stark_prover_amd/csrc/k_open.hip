@@ -16,6 +16,19 @@ __global__ __launch_bounds__(256) void k_open_denoms(Fr z, Fr gen, const Fr* __r
     den[i] = fr_sub(z, fr_mul(gen, pow2l(tabN, L1, brev_bits(row0 + i, logN))));
 }
 
+// 1/(z w_h - x) = w_h^-1 / (z - x w_h^-1), and x w_h^-1 is the domain point
+// `step` = N/h positions earlier in natural order: the inverse denominators of
+// zeta_next are a permuted, scaled copy of zeta's.  Row j = bitrev(bitrev(i) - step)
+// keeps the low log_blowup bits of the natural index, i.e. the same shard.
+__global__ __launch_bounds__(256) void k_shift_inverse(const Fr* __restrict__ inv_z, Fr* __restrict__ out, Fr c,
+                                                       uint32_t logN, uint64_t step, uint64_t row0, size_t n) {
+    const size_t i = gtid();
+    if (i >= n) return;
+    const uint64_t nat = brev_bits(row0 + i, logN);
+    const uint64_t j = brev_bits((nat - step) & ((1ull << logN) - 1), logN) - row0;
+    out[i] = fr_mul(c, inv_z[j]);
+}
+
 constexpr uint32_t INTERP_ROWS = 1024;  // rows per block
 
 // partial[b*w + c] = sum over the block's rows i of M[i][c] * x_i * inv_den[i]
@@ -110,6 +123,12 @@ hipError_t launch_open_denoms(Fr z, Fr gen, const Fr* tabN, uint32_t L1, uint32_
                               hipStream_t st, uint64_t row0) {
     hipLaunchKernelGGL(k_open_denoms, dim3(nblocks(n, 256)), dim3(256), 0, st, z, gen, tabN, L1, logN, n, row0,
                        den);
+    return hipGetLastError();
+}
+
+hipError_t launch_shift_inverse(const Fr* inv_z, Fr* out, Fr c, uint32_t logN, uint64_t step, uint64_t row0, size_t n,
+                                hipStream_t st) {
+    hipLaunchKernelGGL(k_shift_inverse, dim3(nblocks(n, 256)), dim3(256), 0, st, inv_z, out, c, logN, step, row0, n);
     return hipGetLastError();
 }
 

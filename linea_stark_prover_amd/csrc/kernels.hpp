@@ -56,7 +56,11 @@ hipError_t launch_merkle_levels(Fr* layers, size_t nleaves, size_t stop_len, con
 
 // --------------------------------------------------------- k_field.hip
 // out[i] = 1 / in[i] (Montgomery trick, interleaved chunks); in may alias out? no
-hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st);
+// out[i] = 1/in[i] (0 -> 0); out != in.  scratch: batch_inverse_scratch(n)
+// elements (hierarchical, one Fermat inverse per call), or nullptr for the
+// single-level kernel (one inverse per 8..256 elements)
+size_t batch_inverse_scratch(size_t n);
+hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st, Fr* scratch = nullptr);
 // Fr-mul throughput probe: nthreads lanes x iters x 4 independent products
 hipError_t launch_calib_mul(Fr* out, size_t nthreads, uint32_t iters, hipStream_t st);
 // iters chained Poseidon2 permutations per lane, register-resident (k_hash.hip)
@@ -123,6 +127,10 @@ hipError_t launch_quotient(const QuotientArgs& a, hipStream_t st);
 // den[i] = z - GEN * w_N^bitrev(row0 + i) for i < n (two-level table of w_N)
 hipError_t launch_open_denoms(Fr z, Fr gen, const Fr* tabN, uint32_t L1, uint32_t logN, size_t n, Fr* den,
                               hipStream_t st, uint64_t row0 = 0);
+// out[i] = c * inv_z[bitrev(bitrev(row0 + i) - step) - row0], i < n: the
+// inverse denominators at z w_h from those at z (c = w_h^-1, step = N/h)
+hipError_t launch_shift_inverse(const Fr* inv_z, Fr* out, Fr c, uint32_t logN, uint64_t step, uint64_t row0, size_t n,
+                                hipStream_t st);
 // partial sums for barycentric interpolation over rows [0, h):
 // partial[b*w + c] = sum_{i in block b} M[i][c] * x_i * inv_den[i]
 hipError_t launch_interp_partial(const Fr* M, uint32_t w, size_t h, const Fr* inv_den, Fr gen, const Fr* tabN,

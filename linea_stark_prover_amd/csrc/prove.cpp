@@ -343,7 +343,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                 Fr* den = ctx->fbuf("q_den", Sq);
                 inv_den = ctx->fbuf(key, Sq);
                 LSP_HIP(launch_selector_denoms(tabQ, L1Q, GEN, wh_inv, Sq, den, st, i0, logGq));
-                LSP_HIP(launch_batch_inverse(den, inv_den, Sq, st));
+                LSP_HIP(launch_batch_inverse(den, inv_den, Sq, st, ctx->bi_scratch(Sq)));
                 ctx->ptabs[key] = inv_den;
             }
             {
@@ -425,9 +425,8 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         Fr* inv_z = ctx->fbuf("o_invz", S);
         Fr* inv_zn = ctx->fbuf("o_invzn", S);
         LSP_HIP(launch_open_denoms(zeta, GEN, tabN, L1N, logN, S, dtmp, st, row0));
-        LSP_HIP(launch_batch_inverse(dtmp, inv_z, S, st));
-        LSP_HIP(launch_open_denoms(zeta_next, GEN, tabN, L1N, logN, S, dtmp, st, row0));
-        LSP_HIP(launch_batch_inverse(dtmp, inv_zn, S, st));
+        LSP_HIP(launch_batch_inverse(dtmp, inv_z, S, st, ctx->bi_scratch(S)));
+        LSP_HIP(launch_shift_inverse(inv_z, inv_zn, wh_inv, logN, 1ull << lb, row0, S, st));
         T.end("compute_inverse_denominators");
         T.begin("compute opened values with Lagrange interpolation");
         // barycentric sums on the low coset (first h rows: rank 0), then the host-side factor

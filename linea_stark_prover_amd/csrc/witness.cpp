@@ -268,7 +268,7 @@ void witness_permutation_device(lsp_ctx* ctx, const Fr* a, uint32_t na, const Fr
     const size_t sb = witness_scratch_bytes(n, 0);
     void* scratch = ctx->buf("wit_scratch", sb);
     LSP_HIP(launch_perm_rows(a, na, b, nb, n, alpha, delta, out, ostride, al, bl, st));
-    LSP_HIP(launch_batch_inverse(bl, binv, n, st));
+    LSP_HIP(launch_batch_inverse(bl, binv, n, st, ctx->bi_scratch(n)));
     LSP_HIP(launch_mul_vec(al, binv, n, al, st));
     LSP_HIP(launch_fr_scan(al, chk, n, true, scratch, sb, st));
     LSP_HIP(launch_put_col(binv, n, out, ostride, na + nb, st));
@@ -296,7 +296,7 @@ void witness_lookup_device(lsp_ctx* ctx, const Fr* a, uint32_t na, const Fr* b, 
     const size_t sb = witness_scratch_bytes(n, nt);
     void* scratch = ctx->buf("wit_scratch", sb);
     LSP_HIP(launch_lookup_rows(a, na, b, nt, nbc, afil, bfil, n, alpha, delta, out, ostride, comb, den, st));
-    LSP_HIP(launch_batch_inverse(den, inv, m, st));
+    LSP_HIP(launch_batch_inverse(den, inv, m, st, ctx->bi_scratch(m)));
     LSP_HIP(launch_lookup_occurrences(comb, n, nt, afil, bfil, occ, scratch, sb, st));
     const uint32_t col_ainv = na + nt * nbc + 1 + nt;
     LSP_HIP(launch_lookup_terms(inv, occ, afil, n, nt, out, ostride, col_ainv, term, st));

@@ -160,13 +160,20 @@ def test_fri_fold_matches_pyoracle_and_fold_row(gpu_ctx, logn):
 
 
 # ----------------------------------------------------------- batch inverse
-@pytest.mark.parametrize("n", [1, 31, 32, 33, 1000, 70001])
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 1000, 4096, 4097, 70001, (1 << 20) + 3])
 def test_batch_inverse(gpu_ctx, n):
+    """hierarchical Montgomery trick: one-workgroup base (n <= 4096), one and
+    several up/down levels above it"""
     rng = np.random.default_rng(n)
-    x = rand_fr(rng, (n,))
+    m = min(n, 3000)
+    x = rand_fr(rng, (m,))
+    if n > m:  # tile the random block (distinct values are not needed, only nonzero ones)
+        x = np.concatenate([x] * (n // m + 1))[:n]
     inv = gpu_ctx.batch_inverse(x)
-    xi, ii = ints(x), ints(inv)
-    for a, b in zip(xi[:2000], ii[:2000]):
+    idx = sorted(set(range(min(n, 1500))) | set(range(max(0, n - 1500), n)) |
+                 set(rng.integers(0, n, 1000).tolist()))
+    xi, ii = ints(x[idx]), ints(inv[idx])
+    for a, b in zip(xi, ii):
         assert a * b % P == 1
 
 

@@ -190,6 +190,7 @@ int lsp_ctx_destroy(lsp_ctx* ctx) {
     for (auto& kv : ctx->hpool)
         if (kv.second.p) (void)hipHostFree(kv.second.p);
     for (auto& kv : ctx->twiddles) (void)hipFree(kv.second);
+    for (auto& kv : ctx->stage_ev) (void)hipEventDestroy(kv.second);
     if (ctx->rc_dev) (void)hipFree(ctx->rc_dev);
     if (ctx->rc29_dev) (void)hipFree(ctx->rc29_dev);
     (void)hipStreamDestroy(ctx->stream);

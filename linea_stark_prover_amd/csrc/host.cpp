@@ -3,6 +3,7 @@
 #include "host.hpp"
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -10,6 +11,23 @@
 namespace lsp {
 
 Fr host_generator() { return fr_from_u64(22); }
+
+Fr host_inv_cached(const Fr& a) {
+    static std::mutex mu;
+    static std::map<std::array<uint32_t, 8>, Fr> cache;
+    std::array<uint32_t, 8> k;
+    for (int i = 0; i < 8; ++i) k[i] = a.v[i];
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = cache.find(k);
+        if (it != cache.end()) return it->second;
+    }
+    const Fr r = fr_inv(a);
+    std::lock_guard<std::mutex> g(mu);
+    if (cache.size() > 4096) cache.clear();
+    cache[k] = r;
+    return r;
+}
 
 Fr host_two_adic_generator(uint32_t bits) {
     // ROOT_2_47 = 22^((r-1) >> 47); (r-1) >> 47 as 32-bit words
@@ -307,9 +325,29 @@ void* lsp_ctx::hbuf(const std::string& name, size_t bytes) {
     return b.p;
 }
 
+void lsp_ctx::h2d_async(const std::string& name, void* dst, const void* src, size_t bytes) {
+    if (!bytes) return;
+    auto it = stage_ev.find(name);
+    if (it == stage_ev.end()) {
+        hipEvent_t ev;
+        LSP_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        it = stage_ev.emplace(name, ev).first;
+    } else {
+        LSP_HIP(hipEventSynchronize(it->second));
+    }
+    void* h = hbuf(name, bytes);
+    std::memcpy(h, src, bytes);
+    LSP_HIP(hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, stream));
+    LSP_HIP(hipEventRecord(it->second, stream));
+}
+
 lsp::HostPool& lsp_ctx::host_pool() {
     if (!pool_) {
-        unsigned n = std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+        // up to 16 threads (a 1-GPU box's CPU share), fewer when the launcher
+        // says several ranks share this host (torchrun's LOCAL_WORLD_SIZE)
+        unsigned ranks = 1;
+        if (const char* e = std::getenv("LOCAL_WORLD_SIZE")) ranks = (unsigned)std::max(1L, std::strtol(e, nullptr, 10));
+        unsigned n = std::min(16u, std::max(1u, std::thread::hardware_concurrency() / ranks));
         if (const char* e = std::getenv("LSP_HOST_THREADS")) n = (unsigned)std::max(1L, std::strtol(e, nullptr, 10));
         pool_.reset(new lsp::HostPool(n - 1));
     }

@@ -57,6 +57,10 @@ inline lsp_fr from_fr(const Fr& x) {
 // GENERATOR = 22 (U9) and two-adic generators
 Fr host_generator();
 Fr host_two_adic_generator(uint32_t bits);
+// 1/a for the per-shape constants the prover inverts on its critical path
+// (1/h, w^-1, 1/Z_H on the quotient cosets, ...): a process-wide cache, so a
+// proof of a shape seen before spends no host time on Fermat inverses
+Fr host_inv_cached(const Fr& a);
 uint64_t host_bitrev(uint64_t x, uint32_t bits);
 uint32_t log2_exact(size_t n);  // throws LSP_E_SIZE on non-power-of-two
 
@@ -218,6 +222,7 @@ struct lsp_ctx {
     };
     std::map<std::string, Buf> pool;
     std::map<std::string, Buf> hpool;  // pinned host staging buffers (hbuf)
+    std::map<std::string, hipEvent_t> stage_ev;  // last copy out of each h2d_async staging buffer
     std::map<std::pair<uint32_t, int>, lsp::Fr*> twiddles;
     std::map<std::string, const lsp::Fr*> ptabs;  // cached power tables (prove.cpp pow_table), pool-owned
     std::vector<std::pair<std::string, double>> timings;
@@ -228,6 +233,10 @@ struct lsp_ctx {
     lsp::Fr* bi_scratch(size_t n) { return fbuf("bi_scratch", lsp::batch_inverse_scratch(n) + 1); }
     // pinned host memory; growing it first drains the stream (a copy may still read it)
     void* hbuf(const std::string& name, size_t bytes);
+    // asynchronous upload of a small host array through the pinned staging
+    // buffer `name`: the caller's memory may be reused at return and the
+    // stream is not drained (only the previous copy out of `name` is awaited)
+    void h2d_async(const std::string& name, void* dst, const void* src, size_t bytes);
     // w_H^x (or its inverse) for x < H/2, in the 29-bit Montgomery form the NTT multiplies by (k_ntt.hip)
     const lsp::Fr* twiddle29(uint32_t logH, bool inverse);
     lsp::HostPool& host_pool();

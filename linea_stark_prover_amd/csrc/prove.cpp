@@ -109,7 +109,7 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
     for (size_t c = 1; c < w; ++c) shared = shared && fr_eq(shifts_host[c], shifts_host[0]);
     const size_t per_coset = shared ? 1 : w;
     const Fr wN = host_two_adic_generator(logN);
-    const Fr hinv = fr_inv(fr_from_u64(h));
+    const Fr hinv = host_inv_cached(fr_from_u64(h));
     std::vector<Fr> bases((size_t)nk * per_coset), scales((size_t)nk * per_coset, hinv);
     for (uint32_t k = 0; k < nk; ++k) {
         const Fr ck = fr_pow_u64(wN, host_bitrev(k0 + k, added_bits));
@@ -118,17 +118,15 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
     uint32_t L1, L2;
     two_level(logh, L1, L2);
     Fr* dbases = ctx->fbuf("lde_bases", bases.size() * 2);
-    LSP_HIP(hipMemcpyAsync(dbases, bases.data(), bases.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
-    LSP_HIP(hipMemcpyAsync(dbases + bases.size(), scales.data(), scales.size() * sizeof(Fr), hipMemcpyHostToDevice,
-                           st));
+    bases.insert(bases.end(), scales.begin(), scales.end());
+    ctx->h2d_async("lde_bases_h", dbases, bases.data(), bases.size() * sizeof(Fr));
+    const size_t nb = bases.size() / 2;
     const size_t per = (1ull << L1) + (1ull << L2);
-    Fr* tabs = ctx->fbuf("lde_tabs", per * bases.size());
-    LSP_HIP(launch_pow_tables(dbases, bases.size(), L1, L2, dbases + bases.size(), tabs, st));
-    LSP_HIP(launch_to_f29form(tabs, tabs, per * bases.size(), st));  // the NTT multiplies by 29-bit-form factors
+    Fr* tabs = ctx->fbuf("lde_tabs", per * nb);
+    LSP_HIP(launch_pow_tables(dbases, nb, L1, L2, dbases + nb, tabs, st));
+    LSP_HIP(launch_to_f29form(tabs, tabs, per * nb, st));  // the NTT multiplies by 29-bit-form factors
     LSP_HIP(launch_lde(d_in, X, d_out, w, logh, nk, ctx->twiddle29(logh, true), ctx->twiddle29(logh, false), tabs, L1,
                        L2, shared ? 0 : 1, st));
-    // host vectors (bases, scales) must outlive the async copies
-    LSP_HIP(hipStreamSynchronize(st));
 }
 
 // ------------------------------------------------------------- Merkle
@@ -326,7 +324,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         uint32_t L1Q;
         const Fr* tabQ = pow_table(ctx, "tabQ", host_two_adic_generator(logQ), logQ, L1Q);
         const Fr wh = host_two_adic_generator(log_h);
-        const Fr wh_inv = fr_inv(wh);
+        const Fr wh_inv = host_inv_cached(wh);
         Fr* qv = ctx->fbuf("q_values", Q);  // the h x q chunk matrix, on every rank
         Fr* qloc = G == 1 ? qv : ctx->fbuf("q_local", Sq);
         std::vector<Fr> zh(q), izh(q);
@@ -351,16 +349,15 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                 Fr x = one;
                 for (size_t k = 0; k < q; ++k) {
                     zh[k] = fr_sub(fr_mul(gh, x), one);
-                    izh[k] = fr_inv(zh[k]);
+                    izh[k] = host_inv_cached(zh[k]);
                     x = fr_mul(x, gq);
                 }
             }
             Fr* dzh = ctx->fbuf("q_zh", 2 * q);
-            LSP_HIP(hipMemcpyAsync(dzh, zh.data(), q * sizeof(Fr), hipMemcpyHostToDevice, st));
-            LSP_HIP(hipMemcpyAsync(dzh + q, izh.data(), q * sizeof(Fr), hipMemcpyHostToDevice, st));
+            zh.insert(zh.end(), izh.begin(), izh.end());
+            ctx->h2d_async("q_zh_h", dzh, zh.data(), 2 * q * sizeof(Fr));
             int32_t* dair = (int32_t*)ctx->buf("air", air.raw.size() * sizeof(int32_t));
-            LSP_HIP(
-                hipMemcpyAsync(dair, air.raw.data(), air.raw.size() * sizeof(int32_t), hipMemcpyHostToDevice, st));
+            ctx->h2d_async("air_h", dair, air.raw.data(), air.raw.size() * sizeof(int32_t));
             QuotientArgs qa;
             qa.lde = lde;
             qa.w = (uint32_t)w;
@@ -384,7 +381,6 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             qa.row0 = row0;
             qa.n = Sq;
             LSP_HIP(launch_quotient(qa, st));
-            LSP_HIP(hipStreamSynchronize(st));  // zh/izh host vectors
         }
         if (G > 1) {
             // rank r < Gq holds chunks j = bitrev(r) + Gq c as an h x cpr matrix
@@ -396,7 +392,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
 
         // ---- commit to quotient chunks: qv is the h x q matrix of chunks
         T.begin("commit to quotient poly chunks");
-        const Fr gQ = host_two_adic_generator(logQ), gQinv = fr_inv(gQ);
+        const Fr gQ = host_two_adic_generator(logQ), gQinv = host_inv_cached(gQ);
         {
             Fr s = one;
             for (size_t j = 0; j < q; ++j) {
@@ -443,11 +439,11 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)q, sums + 2 * w, st));
         }
         if (G > 1) comm.bcast(ctx, sums, (2 * w + q) * sizeof(Fr), 0);
-        std::vector<Fr> hs(2 * w + q);
-        LSP_HIP(hipMemcpyAsync(hs.data(), sums, hs.size() * sizeof(Fr), hipMemcpyDeviceToHost, st));
+        Fr* hs = (Fr*)ctx->hbuf("o_sums_h", (2 * w + q) * sizeof(Fr));  // pinned
+        LSP_HIP(hipMemcpyAsync(hs, sums, (2 * w + q) * sizeof(Fr), hipMemcpyDeviceToHost, st));
         LSP_HIP(hipStreamSynchronize(st));
         const Fr gh = fr_pow_u64(GEN, h);
-        const Fr dinv = fr_inv(fr_mul(gh, fr_from_u64(h)));
+        const Fr dinv = host_inv_cached(fr_mul(gh, fr_from_u64(h)));
         auto factor = [&](const Fr& z) { return fr_mul(fr_sub(fr_pow_u64(z, h), gh), dinv); };
         const Fr fz = factor(zeta), fzn = factor(zeta_next);
         proof->tl.resize(w);
@@ -470,8 +466,9 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             ry_zn = fr_add(ry_zn, fr_mul(apw[c], proof->tn[c]));
         }
         Fr* dapw = ctx->fbuf("o_apw", apw.size() + q);
-        LSP_HIP(hipMemcpyAsync(dapw, apw.data(), apw.size() * sizeof(Fr), hipMemcpyHostToDevice, st));
-        LSP_HIP(hipMemcpyAsync(dapw + apw.size(), proof->qc.data(), q * sizeof(Fr), hipMemcpyHostToDevice, st));
+        const size_t napw = apw.size();
+        apw.insert(apw.end(), proof->qc.begin(), proof->qc.end());
+        ctx->h2d_async("o_apw_h", dapw, apw.data(), apw.size() * sizeof(Fr));
         // FRI vectors: this rank's slice of round r's input (length (N >> r) / G), back to back
         Fr* fvec = ctx->fbuf("f_vec", 2 * S);
         ReduceArgs ra;
@@ -484,11 +481,10 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         ra.apw = dapw;
         ra.ry_z = ry_z;
         ra.ry_zn = ry_zn;
-        ra.ryq = dapw + apw.size();
+        ra.ryq = dapw + napw;
         ra.out = fvec;
         ra.n = S;
         LSP_HIP(launch_reduce_rows(ra, st));
-        LSP_HIP(hipStreamSynchronize(st));  // apw/qc host vectors
         T.end("reduce rows");
 
         // ---- FRI commit phase
@@ -510,7 +506,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         Fr* fv = fvec;
         size_t len = N, vo = 0, to = 0;
         bool sharded = G > 1;
-        const Fr half = fr_inv(fr_from_u64(2));
+        const Fr half = host_inv_cached(fr_from_u64(2));
         auto replicate = [&]() {  // gather the short vector to every rank
             const size_t loc = len >> b;
             Fr* rep = ctx->fbuf("f_rep", 2 * len);
@@ -534,7 +530,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             const Fr beta = ch.sample();
             uint32_t L1F;
             const uint32_t logm = log2_exact(m);
-            const Fr ginv = fr_inv(host_two_adic_generator(logm + 1));
+            const Fr ginv = host_inv_cached(host_two_adic_generator(logm + 1));
             const Fr* tabF = pow_table(ctx, "tabF", ginv, logm, L1F);
             LSP_HIP(launch_fri_fold(fv + vo, ml, half, fr_mul(beta, half), tabF, L1F, fv + vo + 2 * ml, st,
                                     sharded ? (uint64_t)g * ml : 0, (int)logm));
@@ -545,16 +541,20 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         }
         if (sharded) replicate();
         std::vector<Fr> fin(len);
-        LSP_HIP(hipMemcpyAsync(fin.data(), fv + vo, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
-        LSP_HIP(hipStreamSynchronize(st));
+        {
+            Fr* hf = (Fr*)ctx->hbuf("f_final_h", len * sizeof(Fr));
+            LSP_HIP(hipMemcpyAsync(hf, fv + vo, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
+            LSP_HIP(hipStreamSynchronize(st));
+            std::copy(hf, hf + len, fin.begin());
+        }
         T.end("commit phase");
         {
             // final poly: bit-reverse, IDFT (naive, len <= 2^lb small), truncate
             const uint32_t lgl = log2_exact(len);
             std::vector<Fr> br(len);
             for (size_t i = 0; i < len; ++i) br[i] = fin[host_bitrev(i, lgl)];
-            const Fr winv = fr_inv(host_two_adic_generator(lgl));
-            const Fr linv = fr_inv(fr_from_u64(len));
+            const Fr winv = host_inv_cached(host_two_adic_generator(lgl));
+            const Fr linv = host_inv_cached(fr_from_u64(len));
             const size_t flen = (size_t)1 << ctx->log_final_poly_len;
             for (size_t k = 0; k < len; ++k) {
                 Fr acc = fr_zero();
@@ -619,13 +619,13 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         if (!ptrs.empty()) {
             uint64_t* dptrs = (uint64_t*)ctx->buf("g_ptrs", ptrs.size() * sizeof(uint64_t));
             Fr* dgot = ctx->fbuf("g_out", ptrs.size());
-            LSP_HIP(hipMemcpyAsync(dptrs, ptrs.data(), ptrs.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+            ctx->h2d_async("g_ptrs_h", dptrs, ptrs.data(), ptrs.size() * sizeof(uint64_t));
             LSP_HIP(launch_gather(dptrs, dgot, ptrs.size(), st));
-            std::vector<Fr> got(ptrs.size());
-            LSP_HIP(hipMemcpyAsync(got.data(), dgot, got.size() * sizeof(Fr), hipMemcpyDeviceToHost, st));
+            Fr* got = (Fr*)ctx->hbuf("g_out_h", ptrs.size() * sizeof(Fr));  // pinned: no staging copy
+            LSP_HIP(hipMemcpyAsync(got, dgot, ptrs.size() * sizeof(Fr), hipMemcpyDeviceToHost, st));
             LSP_HIP(hipStreamSynchronize(st));
             for (size_t k = 0; k < mine.size(); ++k)
-                std::copy(got.begin() + k * E, got.begin() + (k + 1) * E, slots.begin() + (size_t)mine[k] * E);
+                std::copy(got + k * E, got + (k + 1) * E, slots.begin() + (size_t)mine[k] * E);
         }
         const std::vector<Fr> all = G > 1 ? comm.allgather_fr(ctx, slots.data(), slots.size()) : slots;
         auto top_path = [&](const std::vector<std::vector<Fr>>& top, size_t sub, std::vector<Fr>& out) {
@@ -684,8 +684,11 @@ struct Writer {
         for (int i = 0; i < 4; ++i) *p++ = (uint8_t)(x >> (8 * i));
     }
     void fr(const Fr& x) {
-        const Fr c = fr_to_canonical(x);
-        for (int i = 0; i < 8; ++i) u32(c.v[i]);
+        // Montgomery form -> integer: a product by 1 on the 4 x 64-bit host multiplier
+        const hp64::F one{{1, 0, 0, 0}};
+        const Fr c = hp64::to_canonical(hp64::mul(hp64::from(x), one));
+        std::memcpy(p, c.v, 32);  // 32-bit words little-endian (x86-64 host)
+        p += 32;
     }
     void frs(const std::vector<Fr>& v) {
         for (auto& x : v) fr(x);

@@ -354,7 +354,7 @@ lsp::HostPool& lsp_ctx::host_pool() {
     return *pool_;
 }
 
-const lsp::Fr* lsp_ctx::twiddle29(uint32_t logH, bool inverse) {
+const uint4* lsp_ctx::twiddle29(uint32_t logH, bool inverse) {
     using namespace lsp;
     auto key = std::make_pair(logH, inverse ? 1 : 0);
     auto it = twiddles.find(key);
@@ -368,10 +368,11 @@ const lsp::Fr* lsp_ctx::twiddle29(uint32_t logH, bool inverse) {
     Fr* base = fbuf("tw_base_tmp", 1);
     LSP_HIP(hipMemcpyAsync(base, &w, sizeof(Fr), hipMemcpyHostToDevice, stream));
     LSP_HIP(launch_pow_tables(base, 1, L1, L2, nullptr, tab, stream));
-    Fr* out = nullptr;
-    LSP_HIP(hipMalloc(&out, half * sizeof(Fr)));
-    LSP_HIP(launch_powers(tab, L1, half, out, stream));
-    LSP_HIP(launch_to_f29form(out, out, half, stream));
+    Fr* pw = fbuf("tw_pow_tmp", half);
+    LSP_HIP(launch_powers(tab, L1, half, pw, stream));
+    uint4* out = nullptr;
+    LSP_HIP(hipMalloc(&out, half * 3 * sizeof(uint4)));
+    LSP_HIP(launch_to_f29limbs(pw, out, half, stream));
     LSP_HIP(hipStreamSynchronize(stream));
     twiddles[key] = out;
     return out;

@@ -223,7 +223,7 @@ struct lsp_ctx {
     std::map<std::string, Buf> pool;
     std::map<std::string, Buf> hpool;  // pinned host staging buffers (hbuf)
     std::map<std::string, hipEvent_t> stage_ev;  // last copy out of each h2d_async staging buffer
-    std::map<std::pair<uint32_t, int>, lsp::Fr*> twiddles;
+    std::map<std::pair<uint32_t, int>, uint4*> twiddles;
     std::map<std::string, const lsp::Fr*> ptabs;  // cached power tables (prove.cpp pow_table), pool-owned
     std::vector<std::pair<std::string, double>> timings;
 
@@ -238,7 +238,7 @@ struct lsp_ctx {
     // stream is not drained (only the previous copy out of `name` is awaited)
     void h2d_async(const std::string& name, void* dst, const void* src, size_t bytes);
     // w_H^x (or its inverse) for x < H/2, in the 29-bit Montgomery form the NTT multiplies by (k_ntt.hip)
-    const lsp::Fr* twiddle29(uint32_t logH, bool inverse);
+    const uint4* twiddle29(uint32_t logH, bool inverse);
     lsp::HostPool& host_pool();
     void sync();
 };

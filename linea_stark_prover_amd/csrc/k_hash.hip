@@ -9,6 +9,8 @@
 // representation (fr29.hpp / poseidon2_f29.hpp: carry-free 64-bit column
 // accumulation, 1.34x the 32-bit-limb permutation rate on MI355X); inputs and
 // digests stay in the ark-ff form.
+#include <cstdlib>
+
 #include "k_common.hpp"
 #include "kernels.hpp"
 #include "poseidon2_f29.hpp"
@@ -167,12 +169,26 @@ hipError_t launch_rc_to_f29(const Fr* rc, F29* rc29, uint32_t n, hipStream_t st)
         }                                                                 \
     } while (0)
 
-static constexpr size_t COOP_MAX = 16384;
+static size_t coop_max() {
+    static const size_t v = [] {
+        const char* e = std::getenv("LSP_COOP_MAX");
+        return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)16384;
+    }();
+    return v;
+}
+static unsigned coop_bs() {
+    static const unsigned v = [] {
+        const char* e = std::getenv("LSP_COOP_BS");
+        return e ? (unsigned)std::strtoul(e, nullptr, 10) : 64u;
+    }();
+    return v;
+}
+#define COOP_MAX coop_max()
 
 // grid for n states: quads in 64-lane blocks when coop, else 256-lane blocks
 static inline void state_grid(size_t n, bool coop, unsigned& blocks, unsigned& bs) {
     if (coop) {
-        bs = 64;
+        bs = coop_bs();
         blocks = nblocks(4 * n, bs);
     } else {
         bs = 256;

@@ -36,7 +36,7 @@ enum PassMode : int { PASS_INPLACE = 0, PASS_INV_FIRST = 1, PASS_FWD_FIRST = 2 }
 struct NttPass {
     const Fr* src;      // PASS_INV_FIRST: caller rows; PASS_FWD_FIRST: X (coefficients)
     Fr* dst;            // the arrays being transformed (h rows each, batch of `narr` arrays, row-major w)
-    const Fr* tw;       // w_H^x (or inverse), x < H/2
+    const uint4* tw;    // w_H^x (or inverse), x < H/2: 29-bit limbs, 3 x uint4 per element
     const Fr* twist;    // PASS_FWD_FIRST: two-level tables per (coset[, column])
     uint32_t L1, L2;    // twist table split
     uint32_t twist_per_col;  // 1: table index k*w + c, 0: table index k
@@ -54,6 +54,16 @@ __device__ __forceinline__ F29 pow2l29(const Fr* tab, uint32_t L1, uint64_t i) {
     return f29_mul(lo, hi);
 }
 
+// 9 limbs from a 48-byte padded slot (two 16-byte loads and one 4-byte load)
+__device__ __forceinline__ F29 f29_load48(const uint4* __restrict__ q) {
+    const uint4 a = q[0], b = q[1];
+    F29 o;
+    o.l[0] = a.x; o.l[1] = a.y; o.l[2] = a.z; o.l[3] = a.w;
+    o.l[4] = b.x; o.l[5] = b.y; o.l[6] = b.z; o.l[7] = b.w;
+    o.l[8] = reinterpret_cast<const uint32_t*>(q + 2)[0];
+    return o;
+}
+
 __device__ __forceinline__ Fr f29_store(const F29& v, bool canon) {
     const Fr o = f29_repack_out(f29_reduce(v));  // < 2r
     return canon ? fr_reduce_once(o) : o;
@@ -61,25 +71,32 @@ __device__ __forceinline__ Fr f29_store(const F29& v, bool canon) {
 
 // One tile: 2^k positions x 2^logG groups x 2^LOGCW columns (power-of-two
 // chunk, so every index below is shifts and masks; rows are 32-bit within
-// an array, H <= 2^31).
+// an array, H <= 2^31).  The first forward pass (PASS_FWD_FIRST) runs one
+// workgroup per tile of the coefficients for ALL cosets: the tile is read
+// from X once into registers (<= 4 elements per thread) and twisted, transformed
+// and stored once per coset, so X is not re-read for every coset.
+constexpr uint32_t NTT_THREADS = 256;
+constexpr uint32_t NTT_MAX_EL = 1024;  // 2^k x G x CW <= 2^7 x 8
+
 template <bool DIF, int MODE, int LOGCW>
-__global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
+__global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
     extern __shared__ F29 lds[];
     constexpr uint32_t CW = 1u << LOGCW;
+    constexpr bool FWD_FIRST = MODE == PASS_FWD_FIRST;
     const uint32_t K = 1u << p.k, logG = p.logG, G = 1u << logG;
     const uint32_t logL = p.logL, Lmask = (1u << logL) - 1, rowshift = logL + p.k;
     const uint64_t H = 1ull << p.logH;
     const uint32_t tiles_per_arr = (uint32_t)(H >> (p.k + logG)) * p.nchunk;
     const uint32_t wg = blockIdx.x;
-    const uint32_t arr = wg / tiles_per_arr;
-    const uint32_t rem = wg - arr * tiles_per_arr;
+    const uint32_t arr0 = FWD_FIRST ? 0u : wg / tiles_per_arr;
+    const uint32_t arr_end = FWD_FIRST ? (uint32_t)p.narr : arr0 + 1;
+    const uint32_t rem = wg - arr0 * tiles_per_arr;
     const uint32_t tile = rem / p.nchunk;
     const uint32_t c0 = (rem - tile * p.nchunk) << LOGCW;
     const uint32_t cw = min(CW, p.w - c0);
     const uint32_t n_el = (K << logG) << LOGCW;
     const bool t_minor = logL < logG;
     const uint32_t gid0 = tile << logG;
-    Fr* base = p.dst + (size_t)arr * H * p.w;
     auto row_of = [&](uint32_t t, uint32_t g) {
         const uint32_t gid = gid0 + g;
         return ((gid >> logL) << rowshift) + (t << logL) + (gid & Lmask);
@@ -95,90 +112,114 @@ __global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
             g = tg & (G - 1);
         }
     };
-    // ---- twist factors s^row / h (29-bit form), once per row when every column shares the shift
+    // ---- first forward pass: this thread's coefficients of the tile, read once
+    constexpr uint32_t NREG = FWD_FIRST ? NTT_MAX_EL / NTT_THREADS : 1;
+    F29 xr[NREG];
+    if (FWD_FIRST) {
+#pragma unroll
+        for (uint32_t j = 0; j < NREG; ++j) {
+            const uint32_t e = threadIdx.x + j * NTT_THREADS;
+            uint32_t t, g, c;
+            split(e, t, g, c);
+            if (e < n_el && c < cw) xr[j] = f29_repack_in(p.src[(size_t)row_of(t, g) * p.w + c0 + c]);
+        }
+    }
     F29* fac = lds + n_el;  // K * G extra entries (launcher sizes the LDS for it)
-    const bool row_twist = MODE == PASS_FWD_FIRST && !p.twist_per_col;
-    if (row_twist) {
-        const Fr* tab = p.twist + (size_t)arr * ((1ull << p.L1) + (1ull << p.L2));
-        for (uint32_t rg = threadIdx.x; rg < (K << logG); rg += blockDim.x) {
-            uint32_t t, g;
-            if (t_minor) {
-                t = rg & (K - 1);
-                g = rg >> p.k;
-            } else {
-                t = rg >> logG;
-                g = rg & (G - 1);
+    const bool row_twist = FWD_FIRST && !p.twist_per_col;
+    for (uint32_t arr = arr0; arr < arr_end; ++arr) {
+        Fr* base = p.dst + (size_t)arr * H * p.w;
+        if (FWD_FIRST && arr > arr0) __syncthreads();  // the previous coset's stores have read the LDS
+        // ---- twist factors s^row / h (29-bit form), once per row when every column shares the shift
+        if (row_twist) {
+            const Fr* tab = p.twist + (size_t)arr * ((1ull << p.L1) + (1ull << p.L2));
+            for (uint32_t rg = threadIdx.x; rg < (K << logG); rg += NTT_THREADS) {
+                uint32_t t, g;
+                if (t_minor) {
+                    t = rg & (K - 1);
+                    g = rg >> p.k;
+                } else {
+                    t = rg >> logG;
+                    g = rg & (G - 1);
+                }
+                fac[(t << logG) + g] = pow2l29(tab, p.L1, row_of(t, g));
             }
-            fac[(t << logG) + g] = pow2l29(tab, p.L1, row_of(t, g));
+            __syncthreads();
         }
-        __syncthreads();
-    }
-    // ---- load (optionally gathering / twisting)
-    for (uint32_t e = threadIdx.x; e < n_el; e += blockDim.x) {
-        uint32_t t, g, c;
-        split(e, t, g, c);
-        if (c >= cw) continue;
-        const uint32_t row = row_of(t, g);
-        F29 v;
-        if (MODE == PASS_INV_FIRST) {
-            v = f29_repack_in(p.src[(size_t)brev_bits(row, p.logH) * p.w + c0 + c]);
-        } else if (MODE == PASS_FWD_FIRST) {
-            F29 f;
-            if (row_twist) {
-                f = fac[(t << logG) + g];
-            } else {
-                const Fr* tab = p.twist + ((size_t)arr * p.w + c0 + c) * ((1ull << p.L1) + (1ull << p.L2));
-                f = pow2l29(tab, p.L1, row);
+        // ---- load (optionally gathering / twisting)
+        if (FWD_FIRST) {
+#pragma unroll
+            for (uint32_t j = 0; j < NREG; ++j) {
+                const uint32_t e = threadIdx.x + j * NTT_THREADS;
+                uint32_t t, g, c;
+                split(e, t, g, c);
+                if (e >= n_el || c >= cw) continue;
+                F29 f;
+                if (row_twist) {
+                    f = fac[(t << logG) + g];
+                } else {
+                    const Fr* tab = p.twist + ((size_t)arr * p.w + c0 + c) * ((1ull << p.L1) + (1ull << p.L2));
+                    f = pow2l29(tab, p.L1, row_of(t, g));
+                }
+                lds[(((t << logG) + g) << LOGCW) + c] = f29_mul(xr[j], f);  // < 8.3 r
             }
-            v = f29_mul(f29_repack_in(p.src[(size_t)row * p.w + c0 + c]), f);  // < 8.3 r
         } else {
-            v = f29_repack_in(base[(size_t)row * p.w + c0 + c]);
-        }
-        lds[(((t << logG) + g) << LOGCW) + c] = v;
-    }
-    __syncthreads();
-    // ---- k radix-2 stages
-    const uint32_t nbf = n_el >> 1;
-    for (uint32_t j = 0; j < p.k; ++j) {
-        const uint32_t s = p.s0 + j;
-        const uint32_t logd = DIF ? (p.k - 1 - j) : j;
-        const bool trivial = DIF ? (s == p.logH - 1) : (s == 0);
-        const uint32_t dmask = (1u << logd) - 1;
-        // twiddle index of butterfly row i0: DIF (i0 mod H/2^(s+1)) << s, DIT (i0 mod 2^s) << (logH-1-s)
-        const uint32_t tmask = DIF ? (uint32_t)((H >> (s + 1)) - 1) : ((1u << s) - 1);
-        const uint32_t tshift = DIF ? s : (p.logH - 1 - s);
-        for (uint32_t bf = threadIdx.x; bf < nbf; bf += blockDim.x) {
-            const uint32_t c = bf & (CW - 1);
-            const uint32_t pg = bf >> LOGCW;
-            const uint32_t g = pg & (G - 1), pp = pg >> logG;
-            const uint32_t t0 = ((pp >> logd) << (logd + 1)) | (pp & dmask);
-            const uint32_t t1 = t0 + (1u << logd);
-            const uint32_t a0 = (((t0 << logG) + g) << LOGCW) + c, a1 = (((t1 << logG) + g) << LOGCW) + c;
-            const F29 a = lds[a0], b = lds[a1];
-            if (trivial) {
-                lds[a0] = f29_reduce(f29_lazy2(a, b));
-                lds[a1] = f29_reduce(f29_sub16(a, b));
-                continue;
-            }
-            const F29 wv = f29_repack_in(p.tw[(row_of(t0, g) & tmask) << tshift]);
-            if (DIF) {
-                lds[a0] = f29_reduce(f29_lazy2(a, b));
-                lds[a1] = f29_mul(f29_sub16(a, b), wv);
-            } else {
-                const F29 bw = f29_mul(b, wv);
-                lds[a0] = f29_reduce(f29_lazy2(a, bw));
-                lds[a1] = f29_reduce(f29_sub16(a, bw));
+            for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
+                uint32_t t, g, c;
+                split(e, t, g, c);
+                if (c >= cw) continue;
+                const uint32_t row = row_of(t, g);
+                F29 v;
+                if (MODE == PASS_INV_FIRST)
+                    v = f29_repack_in(p.src[(size_t)brev_bits(row, p.logH) * p.w + c0 + c]);
+                else
+                    v = f29_repack_in(base[(size_t)row * p.w + c0 + c]);
+                lds[(((t << logG) + g) << LOGCW) + c] = v;
             }
         }
         __syncthreads();
-    }
-    // ---- store
-    const bool canon = p.canon != 0;
-    for (uint32_t e = threadIdx.x; e < n_el; e += blockDim.x) {
-        uint32_t t, g, c;
-        split(e, t, g, c);
-        if (c >= cw) continue;
-        base[(size_t)row_of(t, g) * p.w + c0 + c] = f29_store(lds[(((t << logG) + g) << LOGCW) + c], canon);
+        // ---- k radix-2 stages
+        const uint32_t nbf = n_el >> 1;
+        for (uint32_t j = 0; j < p.k; ++j) {
+            const uint32_t s = p.s0 + j;
+            const uint32_t logd = DIF ? (p.k - 1 - j) : j;
+            const bool trivial = DIF ? (s == p.logH - 1) : (s == 0);
+            const uint32_t dmask = (1u << logd) - 1;
+            // twiddle index of butterfly row i0: DIF (i0 mod H/2^(s+1)) << s, DIT (i0 mod 2^s) << (logH-1-s)
+            const uint32_t tmask = DIF ? (uint32_t)((H >> (s + 1)) - 1) : ((1u << s) - 1);
+            const uint32_t tshift = DIF ? s : (p.logH - 1 - s);
+            for (uint32_t bf = threadIdx.x; bf < nbf; bf += NTT_THREADS) {
+                const uint32_t c = bf & (CW - 1);
+                const uint32_t pg = bf >> LOGCW;
+                const uint32_t g = pg & (G - 1), pp = pg >> logG;
+                const uint32_t t0 = ((pp >> logd) << (logd + 1)) | (pp & dmask);
+                const uint32_t t1 = t0 + (1u << logd);
+                const uint32_t a0 = (((t0 << logG) + g) << LOGCW) + c, a1 = (((t1 << logG) + g) << LOGCW) + c;
+                const F29 a = lds[a0], b = lds[a1];
+                if (trivial) {
+                    lds[a0] = f29_reduce(f29_lazy2(a, b));
+                    lds[a1] = f29_reduce(f29_sub16(a, b));
+                    continue;
+                }
+                const F29 wv = f29_load48(p.tw + 3 * (size_t)((row_of(t0, g) & tmask) << tshift));
+                if (DIF) {
+                    lds[a0] = f29_reduce(f29_lazy2(a, b));
+                    lds[a1] = f29_mul(f29_sub16(a, b), wv);
+                } else {
+                    const F29 bw = f29_mul(b, wv);
+                    lds[a0] = f29_reduce(f29_lazy2(a, bw));
+                    lds[a1] = f29_reduce(f29_sub16(a, bw));
+                }
+            }
+            __syncthreads();
+        }
+        // ---- store
+        const bool canon = p.canon != 0;
+        for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
+            uint32_t t, g, c;
+            split(e, t, g, c);
+            if (c >= cw) continue;
+            base[(size_t)row_of(t, g) * p.w + c0 + c] = f29_store(lds[(((t << logG) + g) << LOGCW) + c], canon);
+        }
     }
 }
 
@@ -187,6 +228,15 @@ __global__ __launch_bounds__(256) void k_ntt_rm(NttPass p) {
 __global__ __launch_bounds__(256) void k_to_f29form(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n) {
     const size_t i = gtid();
     if (i < n) out[i] = f29_store(f29_from_fr(in[i]), true);
+}
+
+__global__ __launch_bounds__(256) void k_to_f29limbs(const Fr* __restrict__ in, uint4* __restrict__ out, size_t n) {
+    const size_t i = gtid();
+    if (i >= n) return;
+    const F29 v = f29_repack_in(f29_store(f29_from_fr(in[i]), true));
+    out[3 * i] = make_uint4(v.l[0], v.l[1], v.l[2], v.l[3]);
+    out[3 * i + 1] = make_uint4(v.l[4], v.l[5], v.l[6], v.l[7]);
+    out[3 * i + 2] = make_uint4(v.l[8], 0u, 0u, 0u);
 }
 
 __global__ __launch_bounds__(256) void k_pow_tables(const Fr* __restrict__ bases, size_t nbases, uint32_t L1,
@@ -223,8 +273,8 @@ void plan_passes(uint32_t logH, uint32_t kmax, uint32_t* ks, uint32_t& np) {
 }
 }  // namespace
 
-hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t ncosets, const Fr* tw_inv,
-                      const Fr* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
+hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t ncosets, const uint4* tw_inv,
+                      const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
                       hipStream_t st) {
     if (w == 0) return hipSuccess;
     // column chunk: the power of two >= min(w, 8); CW * G = 8 (256-byte row runs)
@@ -236,7 +286,7 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
     // k <= 7: a tile of <= 1024 limb-form elements (36 KiB) plus the twist factors
     const uint32_t kmax = 7;
     uint32_t ks[16], np;
-    auto run = [&](bool dif, uint32_t narr, const Fr* src, Fr* dst, const Fr* tw, int first_mode,
+    auto run = [&](bool dif, uint32_t narr, const Fr* src, Fr* dst, const uint4* tw, int first_mode,
                    bool canon_last) -> hipError_t {
         plan_passes(logh, kmax, ks, np);
         uint32_t s0 = 0;
@@ -260,7 +310,9 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
             p.nchunk = nchunk;
             p.canon = (canon_last && q + 1 == np) ? 1u : 0u;
             p.narr = narr;
-            const uint64_t tiles = (uint64_t)narr * ((1ull << logh) >> (k + logG)) * nchunk;
+            // the first forward pass loops over the cosets inside each workgroup
+            const uint64_t tiles = (uint64_t)(dif && q == 0 && first_mode == PASS_FWD_FIRST ? 1 : narr) *
+                                   ((1ull << logh) >> (k + logG)) * nchunk;
             // tile, plus one twist factor per row in the first forward pass
             const size_t lds = ((size_t(1) << (k + logG)) * CW + (size_t(1) << (k + logG))) * sizeof(F29);
             const int mode = q == 0 ? first_mode : PASS_INPLACE;
@@ -310,6 +362,12 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
 hipError_t launch_to_f29form(const Fr* in, Fr* out, size_t n, hipStream_t st) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_to_f29form, dim3(nblocks(n, 256)), dim3(256), 0, st, in, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_to_f29limbs(const Fr* in, uint4* out, size_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_to_f29limbs, dim3(nblocks(n, 256)), dim3(256), 0, st, in, out, n);
     return hipGetLastError();
 }
 

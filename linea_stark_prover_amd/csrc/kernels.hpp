@@ -19,11 +19,14 @@ namespace lsp {
 // twist: two-level tables (L1, L2) of base s and scale 1/h, one per coset
 // (twist_per_col = 0) or per (coset, column) at index k*w + c -- all tables in
 // the 29-bit Montgomery form (launch_to_f29form; k_ntt.hip).
-hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t ncosets, const Fr* tw_inv,
-                      const Fr* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
+hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t ncosets, const uint4* tw_inv,
+                      const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
                       hipStream_t st);
 // ark-form words -> the 29-bit Montgomery form (x 2^261 mod r), canonical, in place allowed
 hipError_t launch_to_f29form(const Fr* in, Fr* out, size_t n, hipStream_t st);
+// the same, unpacked into 9 x 29-bit limbs padded to 48 bytes (3 x uint4 per
+// element): the NTT's twiddle tables, loaded with no repacking
+hipError_t launch_to_f29limbs(const Fr* in, uint4* out, size_t n, hipStream_t st);
 // Two-level power tables: for each base b,
 // tab[b] = {b^j, j < 2^L1} ++ {b^(j 2^L1) * scale[b], j < 2^L2}   (scale nullable)
 hipError_t launch_pow_tables(const Fr* bases, size_t nbases, uint32_t L1, uint32_t L2, const Fr* scale,

@@ -39,8 +39,16 @@ __device__ __forceinline__ constexpr uint32_t p29(int i) {
 }
 
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(LSP_F29_NO_ASM)
-// the same product / square with one asm block per column (tools/gen_fr29mul.py)
+// the same product / square as ONE asm statement (tools/gen_fr29mul.py --block):
+// the compiler puts a conservative s_nop after every asm statement whose result
+// the next instruction reads, ~25 per product with one statement per column
+// (LSP_F29_COLUMNS, gen_fr29mul.py); the single statement has none -- 7 % less
+// single-wave latency (narrow Merkle levels), the same throughput
+#ifdef LSP_F29_COLUMNS
 #include "fr29_mul_gfx950.inc"
+#else
+#include "fr29_mul_gfx950_blk.inc"
+#endif
 #define LSP_F29_USE_ASM 1
 #endif
 

@@ -98,6 +98,70 @@ def gen(kind, chains):
     return out
 
 
+ACC = "v[2:3]"   # block mode: the accumulator lives in a fixed, clobbered VGPR pair
+ACC_LO = "v2"
+
+
+def gen_block(kind):
+    """the whole product as ONE asm statement: the compiler inserts its
+    conservative hazard s_nop after every asm statement whose result the next
+    instruction reads; inside one statement there are none"""
+    sq = kind == "sqr"
+    name = "f29_sqr_asm" if sq else "f29_mul_asm"
+    sig = "(const F29& a)" if sq else "(const F29& a, const F29& b)"
+    out = [f"__device__ __forceinline__ F29 {name}{sig} {{"]
+    out.append("    uint32_t m0, m1, m2, m3, m4, m5, m6, m7, m8;")
+    if sq:
+        out.append("    const uint32_t " + ", ".join(f"d{i} = a.l[{i}] << 1" for i in range(9)) + ";")
+    out.append("    F29 o;")
+    out.append("    uint64_t c;")
+    lines, ins = [], {}
+    first = True
+    for k in range(17):
+        terms = []
+        if sq:
+            for i in range(max(0, k - 8), 9):
+                j = k - i
+                if j < 0 or j > 8 or i >= j:
+                    continue
+                terms.append((f"d{i}", f"a{j}"))
+            if k % 2 == 0 and k // 2 <= 8:
+                terms.append((f"a{k // 2}", f"a{k // 2}"))
+        else:
+            for j in range(max(0, k - 8), min(k, 8) + 1):
+                terms.append((f"a{j}", f"b{k - j}"))
+        for j in range(max(0, k - 8), min(k, 9)):
+            if 1 <= k - j <= 8:
+                terms.append((f"m{j}", f"p{k - j}"))
+        for x, y in terms:
+            src2 = "0" if first else ACC
+            first = False
+            lines.append(f"v_mad_u64_u32 {ACC}, %[c], %[{x}], %[{y}], {src2}")
+            for o in (x, y):
+                if not o.startswith("m"):
+                    ins[o] = True
+        if k < 9:
+            lines.append(f"v_sub_u32 %[m{k}], 0, {ACC_LO}")
+            lines.append(f"v_mad_u64_u32 {ACC}, %[c], %[m{k}], 1, {ACC}")
+            lines.append(f"v_lshrrev_b64 {ACC}, 29, {ACC}")
+        else:
+            lines.append(f"v_and_b32 %[o{k - 9}], %[mask], {ACC_LO}")
+            lines.append(f"v_lshrrev_b64 {ACC}, 29, {ACC}")
+    lines.append(f"v_mov_b32 %[o8], {ACC_LO}")
+    out.append("    asm(")
+    for l in lines:
+        out.append(f'        "{l}\\n\\t"')
+    outs = [f'[m{k}] "=&v"(m{k})' for k in range(9)] + [f'[o{k}] "=&v"(o.l[{k}])' for k in range(9)] + ['[c] "=&s"(c)']
+    out.append("        : " + ", ".join(outs))
+    out.append("        : " + ", ".join([operand(o) for o in ins] + ['[mask] "s"(0x1fffffffu)']))
+    out.append('        : "v2", "v3");')
+    out.append("    (void)c;")
+    out.append("    (void)m0; (void)m1; (void)m2; (void)m3; (void)m4; (void)m5; (void)m6; (void)m7; (void)m8;")
+    out.append("    return o;")
+    out.append("}")
+    return out
+
+
 def bound():
     """worst column sum for normalised inputs and 32-bit quotient digits"""
     a, m, worst, carry = (1 << 29) - 1, (1 << 32) - 1, 0, 0
@@ -141,6 +205,16 @@ def main():
         w = bound_sub16()
         print("worst column sum, (a + 16r - b) * w: < 2^%.3f" % math.log2(w))
         assert w < 1 << 64
+        return
+    if "--block" in sys.argv:
+        out = OUT.replace(".inc", "_blk.inc")
+        lines = ["// GENERATED by tools/gen_fr29mul.py --block -- do not edit by hand.",
+                 "// 29-bit-limb Montgomery product / square on gfx950: FIPS, the whole product one asm",
+                 "// statement (accumulator in the clobbered pair v[2:3]).  Same results as f29_mul / f29_sqr."]
+        lines += gen_block("mul") + [""] + gen_block("sqr")
+        with open(out, "w") as f:
+            f.write("\n".join(lines) + "\n")
+        print("wrote", out)
         return
     chains = int(sys.argv[1]) if len(sys.argv) > 1 else 1
     lines = ["// GENERATED by tools/gen_fr29mul.py -- do not edit by hand.",

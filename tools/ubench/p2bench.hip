@@ -69,6 +69,12 @@ template <int V> __global__ void kperm_lat(Fr* out, const Fr* rc, const F29* rc2
     out[threadIdx.x] = fr_add(fr_add(a, b), c);
 }
 
+__global__ void kcoop_lat(Fr* out, const F29* rc29, int iters) {
+    Fr a = fr_from_u64(threadIdx.x >> 2), b = fr_from_u64((threadIdx.x >> 2) + 1);
+    for (int i = 0; i < iters; ++i) a = compress_f29<11, true>(a, b, rc29, 8, 22);
+    out[threadIdx.x] = a;
+}
+
 static float timeit(void (*f)(void*), void* arg) { return 0; }
 
 int main() {
@@ -130,6 +136,12 @@ int main() {
         (void)hipEventRecord(e1); (void)hipEventSynchronize(e1); float lms; (void)hipEventElapsedTime(&lms, e0, e1);
         printf("%s poseidon2: %.1f M perm/s (x230 = %.1f G mul/s)   single-wave latency %.1f us/perm\n",
                v == 0 ? "32-bit" : "f29   ", mps, mps * 230 / 1e3, lms * 1e3 / 64);
+    }
+    {
+        (void)hipEventRecord(e0);
+        hipLaunchKernelGGL(kcoop_lat, dim3(1), dim3(64), 0, 0, dout, drc29, 64);
+        (void)hipEventRecord(e1); (void)hipEventSynchronize(e1); float lms; (void)hipEventElapsedTime(&lms, e0, e1);
+        printf("f29 quad-coop poseidon2 single-wave latency %.1f us/perm\n", lms * 1e3 / 64);
     }
     return 0;
 }

@@ -27,6 +27,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["k_ntt.hip", "k_hash.hip", "k_field.hip", "k_quotient.hip", "k_open.hip", "k_witness.hip",
            "host.cpp", "prove.cpp", "verify.cpp", "witness.cpp", "cbor.cpp", "comm_ext.cpp", "capi.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
+          # host code: mulx/adcx/adox for the 4 x 64-bit host multiplier (x86-64 with BMI2 + ADX:
+          # the build container and the MI355X hosts)
+          "-Xarch_host", "-mbmi2", "-Xarch_host", "-madx",
           "-Wno-unused-variable", "-I", os.path.join(ROOT, "include")]
 
 

@@ -118,11 +118,26 @@ void HostPool::loop() {
     }
 }
 
+void HostPool::wake() {
+    if (th_.empty()) return;
+    while (busy_.load() != 0) cpu_relax();
+    job_ = nullptr;
+    n_ = 0;
+    next_.store(0);
+    busy_.store((unsigned)th_.size());
+    gen_.fetch_add(1);
+    if (sleepers_.load() != 0) {
+        std::lock_guard<std::mutex> lk(m_);
+        cv_.notify_all();
+    }
+}
+
 void HostPool::parallel_for(size_t n, const std::function<void(size_t)>& f) {
     if (th_.empty() || n < 2) {
         for (size_t i = 0; i < n; ++i) f(i);
         return;
     }
+    while (busy_.load() != 0) cpu_relax();  // a wake() may still be draining
     // the previous job has fully drained (busy_ == 0), so no worker reads these
     job_ = &f;
     n_ = n;

@@ -185,6 +185,10 @@ class HostPool {
     explicit HostPool(unsigned workers);
     ~HostPool();
     void parallel_for(size_t n, const std::function<void(size_t)>& f);
+    // get the workers spinning (they spin kSpinUs for the next job) ahead of a
+    // parallel_for whose data is about to arrive: no condition-variable wake-up
+    // on the critical path
+    void wake();
     unsigned size() const { return (unsigned)th_.size() + 1; }
     static constexpr int kSpinUs = 300;
 
@@ -223,6 +227,7 @@ struct lsp_ctx {
     std::map<std::string, Buf> pool;
     std::map<std::string, Buf> hpool;  // pinned host staging buffers (hbuf)
     std::map<std::string, hipEvent_t> stage_ev;  // last copy out of each h2d_async staging buffer
+    hipEvent_t ev_near = nullptr, ev_top = nullptr;  // tree-top hand-off (prove.cpp commit_device)
     std::map<std::pair<uint32_t, int>, uint4*> twiddles;
     std::map<std::string, const lsp::Fr*> ptabs;  // cached power tables (prove.cpp pow_table), pool-owned
     std::vector<std::pair<std::string, double>> timings;

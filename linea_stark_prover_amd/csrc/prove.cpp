@@ -139,8 +139,23 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
 // The host layers go back to the device (openings gather from device memory)
 // from a pinned staging buffer, without waiting: the next use of the buffer
 // comes after a later synchronisation of the same stream.
+// LSP_TIME_TOPS=1: host-side timing of the tree tops (diagnostic), printed at exit
+struct TopTimes {
+    bool on = std::getenv("LSP_TIME_TOPS") != nullptr;
+    double sync_us = 0, levels_us = 0, first_us = 0;
+    size_t n = 0;
+    ~TopTimes() {
+        if (on && n)
+            std::fprintf(stderr, "[tree tops] %zu trees: wait-for-GPU %.1f us, host levels %.1f us (first level %.1f us) per tree\n",
+                         n, sync_us / n, levels_us / n, first_us / n);
+    }
+};
+static TopTimes g_top_times;
+
 Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers) {
     hipStream_t st = ctx->stream;
+    using clk = std::chrono::steady_clock;
+    const auto tt0 = clk::now();
     size_t top = ctx->host_tree_top;
     if (const char* e = std::getenv("LSP_HOST_TREE_TOP")) top = std::strtoull(e, nullptr, 10);
     HostPool& pool = ctx->host_pool();
@@ -160,20 +175,49 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers) {
             LSP_HIP(launch_merkle_tree(layers, height, ctx->rc29_dev, ctx->p2.L, st));
             return d2h_fr(ctx, layers + 2 * height - 2);
         }
-        LSP_HIP(launch_merkle_levels(layers, height, top, ctx->rc29_dev, ctx->p2.L, &off, &len, st));
+        // all but the last two GPU levels; an event; the last two (~120 us) and the download
+        size_t off1 = 0, len1 = height;
+        LSP_HIP(launch_merkle_levels(layers, height, 4 * top, ctx->rc29_dev, ctx->p2.L, &off1, &len1, st));
+        if (!ctx->ev_near) {
+            LSP_HIP(hipEventCreateWithFlags(&ctx->ev_near, hipEventDisableTiming));
+            LSP_HIP(hipEventCreateWithFlags(&ctx->ev_top, hipEventDisableTiming));
+        }
+        LSP_HIP(hipEventRecord(ctx->ev_near, st));
+        LSP_HIP(launch_merkle_levels(layers + off1, len1, top, ctx->rc29_dev, ctx->p2.L, &off, &len, st));
+        off += off1;
         host = (Fr*)ctx->hbuf("merkle_top", (2 * len - 1) * sizeof(Fr));
         LSP_HIP(hipMemcpyAsync(host, layers + off, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
-        LSP_HIP(hipStreamSynchronize(st));
+        LSP_HIP(hipEventRecord(ctx->ev_top, st));
+        // sleep through the wide levels, then spin (with the pool awake) for the last ones
+        LSP_HIP(hipEventSynchronize(ctx->ev_near));
+        pool.wake();
+        hipError_t q;
+        while ((q = hipEventQuery(ctx->ev_top)) == hipErrorNotReady) {
+#if defined(__x86_64__)
+            __builtin_ia32_pause();
+#endif
+        }
+        LSP_HIP(q);
     }
+    const auto tt1 = clk::now();
+    auto tt2 = tt1;
     const size_t first = len;  // the part already on the device (unless hashed here)
     size_t lo = 0, n = first, end = first;
     while (n > 1) {
         Fr* out = host + end;
         const Fr* in = host + lo;
         pool.parallel_for(n / 2, [&](size_t i) { out[i] = ctx->p2.compress(in[2 * i], in[2 * i + 1]); });
+        if (lo == 0) tt2 = clk::now();
         lo = end;
         end += n / 2;
         n /= 2;
+    }
+    if (g_top_times.on) {
+        const auto tt3 = clk::now();
+        g_top_times.n++;
+        g_top_times.sync_us += std::chrono::duration<double, std::micro>(tt1 - tt0).count();
+        g_top_times.levels_us += std::chrono::duration<double, std::micro>(tt3 - tt1).count();
+        g_top_times.first_us += std::chrono::duration<double, std::micro>(tt2 - tt1).count();
     }
     const size_t skip = leaves_on_host ? 0 : first;  // host-made digests start here
     if (end > skip)

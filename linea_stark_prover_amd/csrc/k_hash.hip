@@ -176,10 +176,10 @@ static size_t coop_max() {
     }();
     return v;
 }
-static unsigned coop_bs() {
+static unsigned coop_bs() {  // 0: by width (state_grid)
     static const unsigned v = [] {
         const char* e = std::getenv("LSP_COOP_BS");
-        return e ? (unsigned)std::strtoul(e, nullptr, 10) : 64u;
+        return e ? (unsigned)std::strtoul(e, nullptr, 10) : 0u;
     }();
     return v;
 }
@@ -188,7 +188,10 @@ static unsigned coop_bs() {
 // grid for n states: quads in 64-lane blocks when coop, else 256-lane blocks
 static inline void state_grid(size_t n, bool coop, unsigned& blocks, unsigned& bs) {
     if (coop) {
-        bs = coop_bs();
+        // 4 lanes per state.  At 16K states (one wave per SIMD of the chip) 64-lane
+        // blocks land two waves on some SIMDs (~2x the level's latency); 256-lane
+        // blocks, one per CU, spread them one per SIMD.  Narrower levels: 64.
+        bs = coop_bs() ? coop_bs() : (4 * n >= 65536 ? 256u : 64u);
         blocks = nblocks(4 * n, bs);
     } else {
         bs = 256;

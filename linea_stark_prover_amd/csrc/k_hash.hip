@@ -63,6 +63,26 @@ __global__ __launch_bounds__(256) void k_hash_rows_multi(MatList ml, size_t nrow
 }
 
 template <uint32_t D, bool COOP>
+__global__ __launch_bounds__(256) void k_fold_hash(FoldSpec f, size_t nleaves, Fr* __restrict__ out,
+                                                   const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
+    const size_t j = COOP ? (gtid() >> 2) : gtid();
+    if (j >= nleaves) return;
+    Fr e[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const size_t i = 2 * j + k;
+        const Fr p = fr_mul(f.half_beta, pow2l(f.tab, f.L1, brev_bits(f.i0 + i, f.logm)));
+        e[k] = fr_add(fr_mul(fr_add(f.half, p), f.v[2 * i]), fr_mul(fr_sub(f.half, p), f.v[2 * i + 1]));
+    }
+    if (!COOP || (threadIdx.x & 3) == 0) {
+        f.vout[2 * j] = e[0];
+        f.vout[2 * j + 1] = e[1];
+    }
+    const Fr d = sponge_f29<D, COOP>([&](uint32_t k) { return e[k]; }, 2, rc, rf, rp);
+    if (!COOP || (threadIdx.x & 3) == 0) out[j] = d;
+}
+
+template <uint32_t D, bool COOP>
 __global__ __launch_bounds__(256) void k_merkle_level(const Fr* __restrict__ src, Fr* __restrict__ dst, size_t nout,
                                                       const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
     const size_t i = COOP ? (gtid() >> 2) : gtid();
@@ -216,6 +236,15 @@ hipError_t launch_hash_rows(const MatList& m, size_t nrows, Fr* out, const F29* 
     else
         LSP_DISPATCH_DC(L, coop, k_hash_rows_multi, dim3(blocks), dim3(bs), 0, st, m, nrows, out, rc, L.rounds_f,
                         L.rounds_p);
+    return hipGetLastError();
+}
+
+hipError_t launch_fold_hash(const FoldSpec& f, size_t nleaves, Fr* out, const F29* rc, P2Layout L, hipStream_t st) {
+    if (!nleaves) return hipSuccess;
+    const bool coop = nleaves <= COOP_MAX;
+    unsigned blocks, bs;
+    state_grid(nleaves, coop, blocks, bs);
+    LSP_DISPATCH_DC(L, coop, k_fold_hash, dim3(blocks), dim3(bs), 0, st, f, nleaves, out, rc, L.rounds_f, L.rounds_p);
     return hipGetLastError();
 }
 

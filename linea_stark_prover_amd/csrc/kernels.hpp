@@ -44,6 +44,19 @@ struct MatList {
 hipError_t launch_rc_to_f29(const Fr* rc, F29* rc29, uint32_t n, hipStream_t st);
 hipError_t launch_permute(Fr* states, size_t n, const F29* rc29, P2Layout L, hipStream_t st);
 // out[i] = hash_iter(concat of row i of every matrix in `m`)
+// FRI fold of the previous round fused into this round's leaf hashing: the
+// folded vector v' (2 n values) is written to `vout` and leaf j = hash_iter(
+// v'[2j], v'[2j+1]) to `out`, with v'[i] = (half + p_i) v[2i] + (half - p_i) v[2i+1],
+// p_i = half_beta * tab^bitrev_logm(i0 + i) (launch_fri_fold's formula)
+struct FoldSpec {
+    const Fr* v;      // the previous round's vector (this rank's slice)
+    Fr* vout;         // where the folded vector goes
+    Fr half, half_beta;
+    const Fr* tab;    // two-level table of w_{2M}^-1
+    uint32_t L1, logm;
+    uint64_t i0;
+};
+hipError_t launch_fold_hash(const FoldSpec& f, size_t nleaves, Fr* out, const F29* rc, P2Layout L, hipStream_t st);
 hipError_t launch_hash_rows(const MatList& m, size_t nrows, Fr* out, const F29* rc29, P2Layout L, hipStream_t st);
 // dst[i] = compress(src[2i], src[2i+1]) for i < nout
 hipError_t launch_merkle_level(const Fr* src, Fr* dst, size_t nout, const F29* rc29, P2Layout L, hipStream_t st);

@@ -152,7 +152,7 @@ struct TopTimes {
 };
 static TopTimes g_top_times;
 
-Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers) {
+Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, const FoldSpec* fold) {
     hipStream_t st = ctx->stream;
     using clk = std::chrono::steady_clock;
     const auto tt0 = clk::now();
@@ -160,6 +160,12 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers) {
     if (const char* e = std::getenv("LSP_HOST_TREE_TOP")) top = std::strtoull(e, nullptr, 10);
     HostPool& pool = ctx->host_pool();
     size_t off = 0, len = height;
+    if (fold && height <= top && height > 1) {
+        // a short vector: materialise the fold, then the host path below hashes it
+        LSP_HIP(launch_fri_fold(fold->v, 2 * height, fold->half, fold->half_beta, fold->tab, fold->L1, fold->vout, st,
+                                fold->i0, (int)fold->logm));
+        fold = nullptr;
+    }
     const bool leaves_on_host = height <= top && m.n == 1 && height > 1;
     Fr* host;  // host layers, starting at device offset `off` (pinned)
     if (leaves_on_host) {
@@ -170,7 +176,10 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers) {
         LSP_HIP(hipStreamSynchronize(st));
         pool.parallel_for(height, [&](size_t i) { host[i] = ctx->p2.hash(&rows[i * w], w); });
     } else {
-        LSP_HIP(launch_hash_rows(m, height, layers, ctx->rc29_dev, ctx->p2.L, st));
+        if (fold)
+            LSP_HIP(launch_fold_hash(*fold, height, layers, ctx->rc29_dev, ctx->p2.L, st));
+        else
+            LSP_HIP(launch_hash_rows(m, height, layers, ctx->rc29_dev, ctx->p2.L, st));
         if (top == 0) {
             LSP_HIP(launch_merkle_tree(layers, height, ctx->rc29_dev, ctx->p2.L, st));
             return d2h_fr(ctx, layers + 2 * height - 2);
@@ -559,15 +568,29 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             vo = 0;
             sharded = false;
         };
+        // round r's fold (by beta_r) runs fused into round r+1's leaf hashing
+        FoldSpec pend{};
+        size_t pend_m = 0;  // folded values (this rank's slice)
+        bool pending = false;
+        auto flush_fold = [&]() {
+            if (!pending) return;
+            LSP_HIP(launch_fri_fold(pend.v, pend_m, pend.half, pend.half_beta, pend.tab, pend.L1,
+                                    pend.vout, st, pend.i0, (int)pend.logm));
+            pending = false;
+        };
         while (len > final_len) {
-            if (sharded && (len >> b) < 2 * FRI_SHARD_MIN) replicate();
+            if (sharded && (len >> b) < 2 * FRI_SHARD_MIN) {
+                flush_fold();  // the gathered vector must exist
+                replicate();
+            }
             const size_t m = len / 2, ml = sharded ? (m >> b) : m;
             FriRound R;
             R.vec = fv + vo;
             R.tree = ftree + to;
             R.ml = ml;
             R.sharded = sharded;
-            const Fr lroot = commit_device(ctx, one_mat(fv + vo, 2), ml, ftree + to);
+            const Fr lroot = commit_device(ctx, one_mat(fv + vo, 2), ml, ftree + to, pending ? &pend : nullptr);
+            pending = false;
             const Fr root = sharded ? shard_root(ctx, comm, lroot, R.top) : lroot;
             proof->roots.push_back(root);
             ch.observe(root);
@@ -576,13 +599,22 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             const uint32_t logm = log2_exact(m);
             const Fr ginv = host_inv_cached(host_two_adic_generator(logm + 1));
             const Fr* tabF = pow_table(ctx, "tabF", ginv, logm, L1F);
-            LSP_HIP(launch_fri_fold(fv + vo, ml, half, fr_mul(beta, half), tabF, L1F, fv + vo + 2 * ml, st,
-                                    sharded ? (uint64_t)g * ml : 0, (int)logm));
+            pend.v = fv + vo;
+            pend.vout = fv + vo + 2 * ml;
+            pend.half = half;
+            pend.half_beta = fr_mul(beta, half);
+            pend.tab = tabF;
+            pend.L1 = L1F;
+            pend.logm = logm;
+            pend.i0 = sharded ? (uint64_t)g * ml : 0;
+            pend_m = ml;
+            pending = true;
             rounds.push_back(std::move(R));
             vo += 2 * ml;
             to += 2 * ml - 1;
             len = m;
         }
+        flush_fold();
         if (sharded) replicate();
         std::vector<Fr> fin(len);
         {

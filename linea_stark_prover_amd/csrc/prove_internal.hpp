@@ -9,7 +9,9 @@ namespace lsp {
 void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added_bits, const Fr* shifts_host,
                 Fr* d_out, uint32_t k0 = 0, uint32_t nk = 0);
 // leaves + every layer into `layers` (2*height - 1); returns the root
-Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers);
+// fold: when set, the leaves are the pairs of the FRI fold it describes (fused
+// into the leaf kernel; m.ptr[0] receives the folded vector)
+Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, const FoldSpec* fold = nullptr);
 lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, const Air& air, const Fr* pub,
                         size_t npub);
 struct Comm;

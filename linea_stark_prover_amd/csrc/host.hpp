@@ -211,7 +211,7 @@ struct lsp_ctx {
     int device = 0;
     lsp::Comm* comm = nullptr;  // attached communicator of a process-per-GPU sharded prove (owned)
     std::unique_ptr<lsp::HostPool> pool_;  // lazily created (host_pool())
-    size_t host_tree_top = 128;             // Merkle levels at or below this many digests run on the host
+    size_t host_tree_top = 256;             // Merkle levels at or below this many digests run on the host (16 threads: ~30 us for the 256 -> 128 level vs ~55 us on the GPU)
     hipStream_t stream = nullptr;
     lsp::P2Host p2;
     lsp::Fr* rc_dev = nullptr;    // round constants, ark form

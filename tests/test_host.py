@@ -118,6 +118,28 @@ def test_host_only_context_rejects_device_calls(host_ctx):
     assert e.value.code == _lib.LSP_E_STATE
 
 
+def test_open_entry_points_validate_then_need_a_gpu(host_ctx, product_lib):
+    """lsp_inverse_denominators / lsp_open_reduce: bad arguments are LSP_E_ARG,
+    well-formed calls on a host-only context LSP_E_STATE (no CPU fallback)"""
+    from linea_stark_prover_amd import _lib
+    from linea_stark_prover_amd.field import to_mont
+    one = to_mont([1])
+    with pytest.raises(_lib.LspError) as e:
+        host_ctx.inverse_denominators(to_mont([5, 7]), 3, to_mont([22]))
+    assert e.value.code == _lib.LSP_E_STATE
+    ro = np.zeros((8, 4), np.uint64)
+    with pytest.raises(_lib.LspError) as e:
+        host_ctx.open_reduce(np.zeros((8, 2, 4), np.uint64), np.zeros((1, 8, 4), np.uint64),
+                             np.zeros((1, 2, 4), np.uint64), one, one, ro)
+    assert e.value.code == _lib.LSP_E_STATE
+    P = ctypes.c_void_p
+    buf = np.zeros((16, 4), np.uint64)
+    ptr = P(buf.ctypes.data)
+    assert product_lib.lsp_inverse_denominators(host_ctx.h, ptr, 0, 3, ptr, ptr, 0) == _lib.LSP_E_ARG
+    assert product_lib.lsp_open_reduce(host_ctx.h, ptr, 8, 1, ptr, ptr, 0, ptr, ptr, ptr, 0) == _lib.LSP_E_ARG
+    assert product_lib.lsp_open_reduce(host_ctx.h, ptr, 8, 1, ptr, None, 1, ptr, ptr, ptr, 0) == _lib.LSP_E_ARG
+
+
 @pytest.mark.parametrize("logn,ncols", [(3, 3), (5, 6), (7, 3)])
 def test_product_verifier_accepts_oracle_proofs(host_ctx, oracle_lib, logn, ncols):
     """The product's CPU verifier (lsp_verify) accepts proofs made by the C

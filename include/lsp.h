@@ -187,6 +187,14 @@ int lsp_inverse_denominators(lsp_ctx *ctx, const lsp_fr *points, size_t npoints,
  * input vector ro (n elements, in/out). */
 int lsp_open_reduce(lsp_ctx *ctx, const lsp_fr *mat, size_t n, size_t w, const lsp_fr *inv_denoms, const lsp_fr *ys,
                     size_t npoints, const lsp_fr *alpha, lsp_fr *alpha_pow_offset, lsp_fr *ro, int mem);
+/* The host side of MerkleTreeMmcs::commit (the tree tops below
+ * host_tree_top digests): CompressionFunctionFromHasher on n pairs
+ * (pairs[2i], pairs[2i+1]) -> out[i], and PaddingFreeSponge::hash_iter of n
+ * rows of width w -> out[i], on the CPU (8 at a time with AVX-512 IFMA when the
+ * CPU has it, else 4 x 64-bit scalar).  Host memory; works on a host-only
+ * context. */
+int lsp_host_compress_batch(const lsp_ctx *ctx, const lsp_fr *pairs, size_t n, lsp_fr *out);
+int lsp_host_hash_rows(const lsp_ctx *ctx, const lsp_fr *rows, size_t n, size_t w, lsp_fr *out);
 /* p3-field batch_multiplicative_inverse */
 int lsp_batch_inverse(lsp_ctx *ctx, const lsp_fr *in, size_t n, lsp_fr *out, int mem);
 

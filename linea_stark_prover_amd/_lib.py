@@ -88,6 +88,8 @@ _SIGS = {
                                                 c_fr_p, ctypes.c_int]),
     "lsp_open_reduce": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, c_fr_p, c_fr_p,
                                        ctypes.c_size_t, c_fr_p, c_fr_p, c_fr_p, ctypes.c_int]),
+    "lsp_host_compress_batch": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, c_fr_p]),
+    "lsp_host_hash_rows": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, c_fr_p]),
     "lsp_batch_inverse": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, c_fr_p, ctypes.c_int]),
     "lsp_prove": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
                                  ctypes.c_size_t, c_fr_p, ctypes.c_size_t, ctypes.c_int,

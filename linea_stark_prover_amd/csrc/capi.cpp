@@ -154,6 +154,7 @@ int lsp_ctx_create(int device, const lsp_params* p, lsp_ctx** out) {
         const size_t nrc = 3 * p->rounds_f + p->rounds_p;
         c->p2.rc.resize(nrc);
         for (size_t i = 0; i < nrc; ++i) c->p2.rc[i] = to_fr(p->round_constants[i]);
+        if (ifma::available()) ifma::prepare(c->p2.rc, c->p2.rc8);
         if (device != LSP_HOST_ONLY) {  // LSP_HOST_ONLY: verifier-only context, no GPU touched
             int n = 0;
             if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw LspError(LSP_E_STATE, "no HIP device");
@@ -516,6 +517,26 @@ int lsp_interpolate_coset(lsp_ctx* ctx, const lsp_fr* lde_bitrev, size_t h, size
         const Fr sh = fr_pow_u64(S, h);
         const Fr f = fr_mul(fr_sub(fr_pow_u64(Z, h), sh), fr_inv(fr_mul(sh, fr_from_u64(h))));
         for (size_t c = 0; c < w; ++c) ys_out[c] = from_fr(fr_mul(hs[c], f));
+    });
+}
+
+int lsp_host_compress_batch(const lsp_ctx* ctx, const lsp_fr* pairs, size_t n, lsp_fr* out) {
+    return guarded(const_cast<lsp_ctx*>(ctx), [&] {
+        LSP_REQUIRE(ctx && (pairs || n == 0) && (out || n == 0), LSP_E_ARG, "bad host_compress arguments");
+        std::vector<Fr> in(2 * n), o(n);
+        for (size_t i = 0; i < 2 * n; ++i) in[i] = to_fr(pairs[i]);
+        ctx->p2.compress_range(in.data(), o.data(), 0, n);
+        for (size_t i = 0; i < n; ++i) out[i] = from_fr(o[i]);
+    });
+}
+
+int lsp_host_hash_rows(const lsp_ctx* ctx, const lsp_fr* rows, size_t n, size_t w, lsp_fr* out) {
+    return guarded(const_cast<lsp_ctx*>(ctx), [&] {
+        LSP_REQUIRE(ctx && w >= 1 && (rows || n == 0) && (out || n == 0), LSP_E_ARG, "bad host_hash_rows arguments");
+        std::vector<Fr> in(n * w), o(n);
+        for (size_t i = 0; i < n * w; ++i) in[i] = to_fr(rows[i]);
+        ctx->p2.hash_range(in.data(), w, o.data(), 0, n);
+        for (size_t i = 0; i < n; ++i) out[i] = from_fr(o[i]);
     });
 }
 

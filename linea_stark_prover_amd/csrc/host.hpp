@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -64,9 +65,25 @@ Fr host_inv_cached(const Fr& a);
 uint64_t host_bitrev(uint64_t x, uint32_t bits);
 uint32_t log2_exact(size_t n);  // throws LSP_E_SIZE on non-power-of-two
 
+// Poseidon2 on the host 8 at a time with AVX-512 IFMA (host_ifma.cpp); only
+// when available() -- the CPU has avx512f + avx512ifma and LSP_HOST_IFMA != 0
+namespace ifma {
+struct alignas(64) Lane8 {  // one 52-bit limb of a value in 8 lanes (a __m512i)
+    uint64_t w[8];
+};
+bool available();
+void prepare(const std::vector<Fr>& rc, std::vector<Lane8>& rc_ifma);
+// out[j] = compress(left[j * stride], right[j * stride]), j < n <= 8
+void compress8(const Fr* left, const Fr* right, size_t stride, Fr* out, int n, const std::vector<Lane8>& rc,
+               const P2Layout& L);
+// out[j] = hash_iter(rows[j * w .. j * w + w)), j < n <= 8
+void hash8(const Fr* rows, size_t w, Fr* out, int n, const std::vector<Lane8>& rc, const P2Layout& L);
+}  // namespace ifma
+
 struct P2Host {
     P2Layout L;
     std::vector<Fr> rc;
+    std::vector<ifma::Lane8> rc8;  // round constants for ifma::, 5 limbs each (empty: scalar only)
     // 4 x 64-bit limbs, lazily reduced (poseidon2_host64.hpp); canonical in and out
     void permute(Fr& s0, Fr& s1, Fr& s2) const { hp64::permute3_rt(s0, s1, s2, rc.data(), L); }
     Fr hash(const Fr* in, size_t n) const;
@@ -74,6 +91,24 @@ struct P2Host {
         Fr s0 = l, s1 = r, s2 = fr_zero();
         permute(s0, s1, s2);
         return s0;
+    }
+    // out[i] = compress(in[2i], in[2i+1]) for i in [i0, i1), 8 at a time when IFMA is there
+    void compress_range(const Fr* in, Fr* out, size_t i0, size_t i1) const {
+        if (rc8.empty()) {
+            for (size_t i = i0; i < i1; ++i) out[i] = compress(in[2 * i], in[2 * i + 1]);
+            return;
+        }
+        for (size_t i = i0; i < i1; i += 8)
+            ifma::compress8(in + 2 * i, in + 2 * i + 1, 2, out + i, (int)std::min<size_t>(8, i1 - i), rc8, L);
+    }
+    // out[i] = hash(rows[i w ..]) for i in [i0, i1)
+    void hash_range(const Fr* rows, size_t w, Fr* out, size_t i0, size_t i1) const {
+        if (rc8.empty()) {
+            for (size_t i = i0; i < i1; ++i) out[i] = hash(rows + i * w, w);
+            return;
+        }
+        for (size_t i = i0; i < i1; i += 8)
+            ifma::hash8(rows + i * w, w, out + i, (int)std::min<size_t>(8, i1 - i), rc8, L);
     }
 };
 

@@ -174,7 +174,9 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
         Fr* rows = host + 2 * height - 1;
         LSP_HIP(hipMemcpyAsync(rows, m.ptr[0], height * w * sizeof(Fr), hipMemcpyDeviceToHost, st));
         LSP_HIP(hipStreamSynchronize(st));
-        pool.parallel_for(height, [&](size_t i) { host[i] = ctx->p2.hash(&rows[i * w], w); });
+        pool.parallel_for((height + 7) / 8, [&](size_t b) {
+            ctx->p2.hash_range(rows, w, host, 8 * b, std::min(height, 8 * b + 8));
+        });
     } else {
         if (fold)
             LSP_HIP(launch_fold_hash(*fold, height, layers, ctx->rc29_dev, ctx->p2.L, st));
@@ -215,7 +217,13 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
     while (n > 1) {
         Fr* out = host + end;
         const Fr* in = host + lo;
-        pool.parallel_for(n / 2, [&](size_t i) { out[i] = ctx->p2.compress(in[2 * i], in[2 * i + 1]); });
+        const size_t half = n / 2;
+        if (half <= pool.size())  // one permutation per thread: the scalar path's latency is lower
+            pool.parallel_for(half, [&](size_t i) { out[i] = ctx->p2.compress(in[2 * i], in[2 * i + 1]); });
+        else  // 8 at a time (AVX-512 IFMA when the CPU has it)
+            pool.parallel_for((half + 7) / 8, [&](size_t b) {
+                ctx->p2.compress_range(in, out, 8 * b, std::min(half, 8 * b + 8));
+            });
         if (lo == 0) tt2 = clk::now();
         lo = end;
         end += n / 2;

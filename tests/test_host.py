@@ -118,6 +118,50 @@ def test_host_only_context_rejects_device_calls(host_ctx):
     assert e.value.code == _lib.LSP_E_STATE
 
 
+def _host_merkle_checks(product_lib, ctx, pp, seed):
+    """lsp_host_compress_batch / lsp_host_hash_rows (the tree-top path) vs the oracle"""
+    from linea_stark_prover_amd.field import from_mont, to_mont
+    rng = np.random.default_rng(seed)
+    for n in (1, 7, 8, 9, 37):
+        vals = [int.from_bytes(rng.bytes(32), "little") % O.P for _ in range(2 * n)]
+        pairs, out = to_mont(vals), np.zeros((n, 4), np.uint64)
+        assert product_lib.lsp_host_compress_batch(ctx.h, ctypes.c_void_p(pairs.ctypes.data), n,
+                                                   ctypes.c_void_p(out.ctypes.data)) == 0
+        assert from_mont(out) == [O.compress(vals[2 * i], vals[2 * i + 1], pp) for i in range(n)]
+    for n, w in ((5, 8), (9, 3), (16, 1), (3, 14)):
+        vals = [int.from_bytes(rng.bytes(32), "little") % O.P for _ in range(n * w)]
+        rows, out = to_mont(vals), np.zeros((n, 4), np.uint64)
+        assert product_lib.lsp_host_hash_rows(ctx.h, ctypes.c_void_p(rows.ctypes.data), n, w,
+                                              ctypes.c_void_p(out.ctypes.data)) == 0
+        assert from_mont(out) == [O.hash_iter(vals[i * w:(i + 1) * w], pp) for i in range(n)]
+
+
+def test_host_merkle_path_matches_oracle(host_ctx, product_lib):
+    """the context's host Poseidon2 (AVX-512 IFMA, 8 lanes, when the CPU has it)"""
+    _host_merkle_checks(product_lib, host_ctx, O.setup_from_seed().perm, 1)
+
+
+def test_host_merkle_path_scalar_and_sbox17(product_lib, tmp_path):
+    """the scalar 4 x 64-bit path (LSP_HOST_IFMA=0, read once per process: a child
+    process) and the x^17 S-box on both paths"""
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from tests.test_host import _host_merkle_checks\n"
+        "from oracle import pyoracle as O\n"
+        "from linea_stark_prover_amd import _lib\n"
+        "from linea_stark_prover_amd.prover import Context, StarkConfig\n"
+        "for d in (11, 17):\n"
+        "    ctx = Context(StarkConfig(sbox_degree=d), device=-1)\n"
+        "    _host_merkle_checks(_lib.lib(), ctx, O.setup_from_seed(sbox_degree=d).perm, d)\n"
+    ) % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),)
+    for flag in ("0", "1"):
+        env = dict(os.environ, LSP_HOST_IFMA=flag)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+
+
 def test_open_entry_points_validate_then_need_a_gpu(host_ctx, product_lib):
     """lsp_inverse_denominators / lsp_open_reduce: bad arguments are LSP_E_ARG,
     well-formed calls on a host-only context LSP_E_STATE (no CPU fallback)"""

@@ -8,7 +8,7 @@
 #include <random>
 #include <vector>
 
-#include "poseidon2_host64.hpp"
+#include "host.hpp"
 using namespace lsp;
 
 static Fr rnd(std::mt19937_64& g) {
@@ -18,7 +18,11 @@ static Fr rnd(std::mt19937_64& g) {
     return x;
 }
 
+int bench_ifma();
 int main() {
+#ifdef LSP_BENCH_IFMA
+    if (bench_ifma()) return 1;
+#endif
     std::mt19937_64 g(7);
     std::vector<Fr> rc(46);
     for (auto& c : rc) c = rnd(g);
@@ -41,3 +45,35 @@ int main() {
     printf("host permutation: generic %.2f us, 64-bit lazy %.2f us, mismatches %d (%08x)\n", us[0], us[1], bad, s0.v[0]);
     return bad != 0;
 }
+
+// IFMA batch (tools/ubench: build with host_ifma.cpp, see the header comment):
+// latency of one 8-lane compression vs one scalar compression
+#ifdef LSP_BENCH_IFMA
+#include <vector>
+int bench_ifma() {
+    std::mt19937_64 g(9);
+    std::vector<Fr> rc(46);
+    for (auto& c : rc) c = rnd(g);
+    P2Layout L{8, 22, 11};
+    if (!ifma::available()) { printf("no avx512ifma\n"); return 0; }
+    std::vector<ifma::Lane8> rc8;
+    ifma::prepare(rc, rc8);
+    P2Host p{L, rc, {}};
+    P2Host q{L, rc, rc8};
+    Fr in[16], out[8], ref[8];
+    for (auto& x : in) x = rnd(g);
+    p.compress_range(in, ref, 0, 8);
+    q.compress_range(in, out, 0, 8);
+    int bad = 0;
+    for (int j = 0; j < 8; ++j) bad += !fr_eq(out[j], ref[j]);
+    const int N = 20000;
+    auto t = std::chrono::steady_clock::now();
+    for (int i = 0; i < N; ++i) { q.compress_range(in, out, 0, 8); in[0] = out[3]; }
+    double us8 = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count() / N;
+    t = std::chrono::steady_clock::now();
+    for (int i = 0; i < N; ++i) { in[0] = p.compress(in[0], in[1]); }
+    double us1 = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count() / N;
+    printf("host compression: scalar %.2f us each; IFMA %.2f us per 8 (%.2f us each), mismatches %d\n", us1, us8, us8 / 8, bad);
+    return bad;
+}
+#endif

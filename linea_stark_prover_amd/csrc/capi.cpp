@@ -192,6 +192,7 @@ int lsp_ctx_destroy(lsp_ctx* ctx) {
         if (kv.second.p) (void)hipHostFree(kv.second.p);
     for (auto& kv : ctx->twiddles) (void)hipFree(kv.second);
     for (auto& kv : ctx->stage_ev) (void)hipEventDestroy(kv.second);
+    for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->ev_near) (void)hipEventDestroy(ctx->ev_near);
     if (ctx->ev_top) (void)hipEventDestroy(ctx->ev_top);
     if (ctx->rc_dev) (void)hipFree(ctx->rc_dev);

@@ -263,6 +263,7 @@ struct lsp_ctx {
     std::map<std::string, Buf> hpool;  // pinned host staging buffers (hbuf)
     std::map<std::string, hipEvent_t> stage_ev;  // last copy out of each h2d_async staging buffer
     hipEvent_t ev_near = nullptr, ev_top = nullptr;  // tree-top hand-off (prove.cpp commit_device)
+    std::vector<hipEvent_t> event_pool;               // phase-timer events, reused across proofs
     std::map<std::pair<uint32_t, int>, uint4*> twiddles;
     std::map<std::string, const lsp::Fr*> ptabs;  // cached power tables (prove.cpp pow_table), pool-owned
     std::vector<std::pair<std::string, double>> timings;

@@ -18,22 +18,33 @@
 namespace lsp {
 
 namespace {
+// HIP events around each phase (span names as in the reference's bench.log),
+// taken from and returned to the context's event pool: creating and destroying
+// ~40 events per proof cost ~60 us of host time at the end of every proof
 struct PhaseTimer {
     lsp_ctx* ctx;
     std::vector<std::pair<std::string, hipEvent_t>> starts;
     std::vector<std::tuple<std::string, hipEvent_t, hipEvent_t>> done;
     explicit PhaseTimer(lsp_ctx* c) : ctx(c) {}
-    void begin(const std::string& name) {
+    hipEvent_t take() {
         hipEvent_t e;
-        LSP_HIP(hipEventCreate(&e));
+        if (!ctx->event_pool.empty()) {
+            e = ctx->event_pool.back();
+            ctx->event_pool.pop_back();
+        } else {
+            LSP_HIP(hipEventCreate(&e));
+        }
+        return e;
+    }
+    void begin(const std::string& name) {
+        const hipEvent_t e = take();
         LSP_HIP(hipEventRecord(e, ctx->stream));
         starts.emplace_back(name, e);
     }
     void end(const std::string& name) {
         for (size_t i = starts.size(); i-- > 0;) {
             if (starts[i].first == name) {
-                hipEvent_t e;
-                LSP_HIP(hipEventCreate(&e));
+                const hipEvent_t e = take();
                 LSP_HIP(hipEventRecord(e, ctx->stream));
                 done.emplace_back(name, starts[i].second, e);
                 starts.erase(starts.begin() + i);
@@ -48,10 +59,10 @@ struct PhaseTimer {
             float ms = 0;
             LSP_HIP(hipEventElapsedTime(&ms, std::get<1>(t), std::get<2>(t)));
             ctx->timings.emplace_back(std::get<0>(t), (double)ms);
-            (void)hipEventDestroy(std::get<1>(t));
-            (void)hipEventDestroy(std::get<2>(t));
+            ctx->event_pool.push_back(std::get<1>(t));
+            ctx->event_pool.push_back(std::get<2>(t));
         }
-        for (auto& s : starts) (void)hipEventDestroy(s.second);
+        for (auto& st : starts) ctx->event_pool.push_back(st.second);
         done.clear();
         starts.clear();
     }
@@ -664,10 +675,12 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         // openings below the rank subtrees in one kernel; the layers above come
         // from the host top trees every rank holds.
         T.begin("query phase");
+        const auto q0 = std::chrono::steady_clock::now();
         const uint32_t nr = (uint32_t)rounds.size();
         const uint32_t nq = ctx->num_queries;
         std::vector<size_t> idxs(nq);
         for (uint32_t qi = 0; qi < nq; ++qi) idxs[qi] = (size_t)ch.sample_bits(logN);
+        const auto q1 = std::chrono::steady_clock::now();
         size_t E = w + logS + q + logS;  // elements per query below the rank subtrees
         for (const FriRound& R : rounds) E += 1 + log2_exact(R.ml);
         std::vector<uint64_t> ptrs;
@@ -711,6 +724,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             for (size_t k = 0; k < mine.size(); ++k)
                 std::copy(got + k * E, got + (k + 1) * E, slots.begin() + (size_t)mine[k] * E);
         }
+        const auto q2 = std::chrono::steady_clock::now();
         const std::vector<Fr> all = G > 1 ? comm.allgather_fr(ctx, slots.data(), slots.size()) : slots;
         auto top_path = [&](const std::vector<std::vector<Fr>>& top, size_t sub, std::vector<Fr>& out) {
             for (uint32_t i = 0; i + 1 < top.size(); ++i) out.push_back(top[i][(sub >> i) ^ 1]);
@@ -740,11 +754,13 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             }
             proof->queries.push_back(std::move(qq));
         }
+        const auto q3 = std::chrono::steady_clock::now();
         T.end("query phase");
         T.end("FRI prover");
         T.end("open");
         T.end("prove");
         T.collect();
+        if (g_top_times.on) { const auto q4 = std::chrono::steady_clock::now(); std::fprintf(stderr, "[query] samples %.1f us, gather+sync %.1f us, assemble %.1f us, collect %.1f us\n", std::chrono::duration<double, std::micro>(q1 - q0).count(), std::chrono::duration<double, std::micro>(q2 - q1).count(), std::chrono::duration<double, std::micro>(q3 - q2).count(), std::chrono::duration<double, std::micro>(q4 - q3).count()); }
     } catch (...) {
         delete proof;
         throw;

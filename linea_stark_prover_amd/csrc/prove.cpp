@@ -119,23 +119,39 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
     bool shared = true;
     for (size_t c = 1; c < w; ++c) shared = shared && fr_eq(shifts_host[c], shifts_host[0]);
     const size_t per_coset = shared ? 1 : w;
-    const Fr wN = host_two_adic_generator(logN);
-    const Fr hinv = host_inv_cached(fr_from_u64(h));
-    std::vector<Fr> bases((size_t)nk * per_coset), scales((size_t)nk * per_coset, hinv);
-    for (uint32_t k = 0; k < nk; ++k) {
-        const Fr ck = fr_pow_u64(wN, host_bitrev(k0 + k, added_bits));
-        for (size_t c = 0; c < per_coset; ++c) bases[k * per_coset + c] = fr_mul(shifts_host[c], ck);
-    }
     uint32_t L1, L2;
     two_level(logh, L1, L2);
-    Fr* dbases = ctx->fbuf("lde_bases", bases.size() * 2);
-    bases.insert(bases.end(), scales.begin(), scales.end());
-    ctx->h2d_async("lde_bases_h", dbases, bases.data(), bases.size() * sizeof(Fr));
-    const size_t nb = bases.size() / 2;
     const size_t per = (1ull << L1) + (1ull << L2);
-    Fr* tabs = ctx->fbuf("lde_tabs", per * nb);
-    LSP_HIP(launch_pow_tables(dbases, nb, L1, L2, dbases + nb, tabs, st));
-    LSP_HIP(launch_to_f29form(tabs, tabs, per * nb, st));  // the NTT multiplies by 29-bit-form factors
+    const size_t nb = (size_t)nk * per_coset;
+    // the twist tables depend on the shape and the shifts only: built once per
+    // (log h, cosets, shifts) and kept in the context (pool-owned)
+    uint64_t hsh = 1469598103934665603ull;  // FNV-1a over the shifts' words
+    for (size_t c = 0; c < per_coset; ++c)
+        for (int i = 0; i < 8; ++i) hsh = (hsh ^ shifts_host[c].v[i]) * 1099511628211ull;
+    char key[112];
+    std::snprintf(key, sizeof key, "ldetw_%u_%u_%u_%u_%zu_%016llx", logh, added_bits, k0, nk, per_coset,
+                  (unsigned long long)hsh);
+    const Fr* tabs;
+    auto it = ctx->ptabs.find(key);
+    if (it != ctx->ptabs.end()) {
+        tabs = it->second;
+    } else {
+        const Fr wN = host_two_adic_generator(logN);
+        const Fr hinv = host_inv_cached(fr_from_u64(h));
+        std::vector<Fr> bases(2 * nb, hinv);  // nb bases, then nb scales (1/h)
+        for (uint32_t k = 0; k < nk; ++k) {
+            const Fr ck = fr_pow_u64(wN, host_bitrev(k0 + k, added_bits));
+            for (size_t c = 0; c < per_coset; ++c) bases[k * per_coset + c] = fr_mul(shifts_host[c], ck);
+        }
+        Fr* dbases = ctx->fbuf("lde_bases", 2 * nb);
+        ctx->h2d_async("lde_bases_h", dbases, bases.data(), bases.size() * sizeof(Fr));
+        const bool keep = ctx->ptabs.size() < 256;  // API callers with ever new shifts: a scratch table
+        Fr* t = ctx->fbuf(keep ? key : "lde_tabs", per * nb);
+        LSP_HIP(launch_pow_tables(dbases, nb, L1, L2, dbases + nb, t, st));
+        LSP_HIP(launch_to_f29form(t, t, per * nb, st));  // the NTT multiplies by 29-bit-form factors
+        if (keep) ctx->ptabs[key] = t;
+        tabs = t;
+    }
     LSP_HIP(launch_lde(d_in, X, d_out, w, logh, nk, ctx->twiddle29(logh, true), ctx->twiddle29(logh, false), tabs, L1,
                        L2, shared ? 0 : 1, st));
 }

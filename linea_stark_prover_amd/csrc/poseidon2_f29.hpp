@@ -175,15 +175,20 @@ __device__ __forceinline__ void permute3_any(F29& s0, F29& s1, F29& s2, const F2
 template <uint32_t D, bool COOP = false, class Get>
 __device__ __forceinline__ Fr sponge_f29(Get get, uint32_t n, const F29* rc29, uint32_t rf, uint32_t rp) {
     F29 s0 = f29_zero(), s1 = f29_zero(), s2 = f29_zero();
+    // the next block is loaded before the current permutation, so its memory
+    // latency hides behind ~46 K instructions instead of stalling the wave
+    Fr n0 = n > 0 ? get(0) : fr_zero(), n1 = n > 1 ? get(1) : fr_zero();
     uint32_t k = 0;
     while (k + 2 <= n) {
-        s0 = f29_from_fr(get(k));
-        s1 = f29_from_fr(get(k + 1));
+        s0 = f29_from_fr(n0);
+        s1 = f29_from_fr(n1);
+        if (k + 2 < n) n0 = get(k + 2);
+        if (k + 3 < n) n1 = get(k + 3);
         permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp);
         k += 2;
     }
     if (k < n) {
-        s0 = f29_from_fr(get(k));
+        s0 = f29_from_fr(n0);
         permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp);
     }
     return f29_to_fr(s0);

@@ -17,7 +17,15 @@ def calls(d):
     """group dispatches into LDE calls: a call is its twist-table kernel (k_pow_tables)
     followed by the NTT passes (k_ntt_rm), up to the next call"""
     ks = sorted(d)
-    starts = [k for k in ks if 'k_pow_tables' in d[k][0]]
+    # a call starts at its first inverse pass (k_ntt_rm<false, 1, ...>: PASS_INV_FIRST),
+    # or at the twist-table kernels right before it (absent once the tables are cached)
+    starts = []
+    for i, k in enumerate(ks):
+        if 'k_ntt_rm<false, 1' in d[k][0]:
+            j = i
+            while j > 0 and any(x in d[ks[j - 1]][0] for x in ('k_pow_tables', 'k_to_f29form')):
+                j -= 1
+            starts.append(ks[j])
     out = []
     for i, s in enumerate(starts):
         end = starts[i + 1] if i + 1 < len(starts) else ks[-1] + 1

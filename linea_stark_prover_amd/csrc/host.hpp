@@ -76,6 +76,9 @@ void prepare(const std::vector<Fr>& rc, std::vector<Lane8>& rc_ifma);
 // out[j] = compress(left[j * stride], right[j * stride]), j < n <= 8
 void compress8(const Fr* left, const Fr* right, size_t stride, Fr* out, int n, const std::vector<Lane8>& rc,
                const P2Layout& L);
+// the same for n <= 16, as two 8-lane states in lockstep
+void compress16(const Fr* left, const Fr* right, size_t stride, Fr* out, int n, const std::vector<Lane8>& rc,
+                const P2Layout& L);
 // out[j] = hash_iter(rows[j * w .. j * w + w)), j < n <= 8
 void hash8(const Fr* rows, size_t w, Fr* out, int n, const std::vector<Lane8>& rc, const P2Layout& L);
 }  // namespace ifma
@@ -92,14 +95,16 @@ struct P2Host {
         permute(s0, s1, s2);
         return s0;
     }
-    // out[i] = compress(in[2i], in[2i+1]) for i in [i0, i1), 8 at a time when IFMA is there
+    // out[i] = compress(in[2i], in[2i+1]) for i in [i0, i1), 16 or 8 at a time when IFMA is there
     void compress_range(const Fr* in, Fr* out, size_t i0, size_t i1) const {
         if (rc8.empty()) {
             for (size_t i = i0; i < i1; ++i) out[i] = compress(in[2 * i], in[2 * i + 1]);
             return;
         }
-        for (size_t i = i0; i < i1; i += 8)
-            ifma::compress8(in + 2 * i, in + 2 * i + 1, 2, out + i, (int)std::min<size_t>(8, i1 - i), rc8, L);
+        size_t i = i0;
+        for (; i + 8 < i1; i += 16)  // two states in lockstep: ~10 % more per thread than 8 at a time
+            ifma::compress16(in + 2 * i, in + 2 * i + 1, 2, out + i, (int)std::min<size_t>(16, i1 - i), rc8, L);
+        if (i < i1) ifma::compress8(in + 2 * i, in + 2 * i + 1, 2, out + i, (int)(i1 - i), rc8, L);
     }
     // out[i] = hash(rows[i w ..]) for i in [i0, i1)
     void hash_range(const Fr* rows, size_t w, Fr* out, size_t i0, size_t i1) const {

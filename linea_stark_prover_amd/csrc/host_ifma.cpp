@@ -146,22 +146,6 @@ LSP_IFMA V add(const V& a, const V& b) {
     return csub(s, R2L);
 }
 
-template <uint32_t D>
-LSP_IFMA V sbox(const V& x) {
-    const V x2 = mul(x, x);
-    const V x4 = mul(x2, x2);
-    const V x8 = mul(x4, x4);
-    if (D == 11) return mul(mul(x8, x2), x);
-    return mul(mul(x8, x8), x);  // x^17
-}
-
-LSP_IFMA void ext_layer(V& s0, V& s1, V& s2) {
-    const V t = add(add(s0, s1), s2);
-    s0 = add(s0, t);
-    s1 = add(s1, t);
-    s2 = add(s2, t);
-}
-
 // ark-form words (8 lanes; lane j at src[j * stride]) -> IFMA form
 LSP_IFMA V load(const Fr* src, size_t stride, int n) {
     alignas(64) uint64_t t[5][8];
@@ -194,31 +178,58 @@ LSP_IFMA void store(const V& x, Fr* dst, size_t stride, int n) {
     }
 }
 
-template <uint32_t D>
-LSP_IFMA void permute(V& s0, V& s1, V& s2, const V* rc, uint32_t rounds_f, uint32_t rounds_p) {
+// two independent 8-lane states in lockstep: the dependent IFMA chains of one
+// product leave the multiply pipes partly idle, the other state's fill them
+struct W {
+    V x, y;
+};
+LSP_IFMA W mul(const W& a, const W& b) { return W{mul(a.x, b.x), mul(a.y, b.y)}; }
+LSP_IFMA W add(const W& a, const W& b) { return W{add(a.x, b.x), add(a.y, b.y)}; }
+LSP_IFMA W add(const W& a, const V& c) { return W{add(a.x, c), add(a.y, c)}; }
+
+template <uint32_t D, class T>
+LSP_IFMA T sbox_t(const T& x) {
+    const T x2 = mul(x, x);
+    const T x4 = mul(x2, x2);
+    const T x8 = mul(x4, x4);
+    if (D == 11) return mul(mul(x8, x2), x);
+    return mul(mul(x8, x8), x);  // x^17
+}
+
+template <class T>
+LSP_IFMA void ext_layer_t(T& s0, T& s1, T& s2) {
+    const T t = add(add(s0, s1), s2);
+    s0 = add(s0, t);
+    s1 = add(s1, t);
+    s2 = add(s2, t);
+}
+
+// T = V (8 states) or W (16 states); round constants broadcast in V
+template <uint32_t D, class T>
+LSP_IFMA void permute(T& s0, T& s1, T& s2, const V* rc, uint32_t rounds_f, uint32_t rounds_p) {
     const uint32_t half = rounds_f / 2;
     const V* ini = rc;
     const V* ter = rc + 3 * half;
     const V* itl = rc + 6 * half;
-    ext_layer(s0, s1, s2);
+    ext_layer_t(s0, s1, s2);
     for (uint32_t r = 0; r < half; ++r) {
-        s0 = sbox<D>(add(s0, ini[3 * r + 0]));
-        s1 = sbox<D>(add(s1, ini[3 * r + 1]));
-        s2 = sbox<D>(add(s2, ini[3 * r + 2]));
-        ext_layer(s0, s1, s2);
+        s0 = sbox_t<D>(add(s0, ini[3 * r + 0]));
+        s1 = sbox_t<D>(add(s1, ini[3 * r + 1]));
+        s2 = sbox_t<D>(add(s2, ini[3 * r + 2]));
+        ext_layer_t(s0, s1, s2);
     }
     for (uint32_t r = 0; r < rounds_p; ++r) {
-        s0 = sbox<D>(add(s0, itl[r]));
-        const V t = add(add(s0, s1), s2);
+        s0 = sbox_t<D>(add(s0, itl[r]));
+        const T t = add(add(s0, s1), s2);
         s0 = add(s0, t);
         s1 = add(s1, t);
         s2 = add(add(s2, s2), t);
     }
     for (uint32_t r = 0; r < half; ++r) {
-        s0 = sbox<D>(add(s0, ter[3 * r + 0]));
-        s1 = sbox<D>(add(s1, ter[3 * r + 1]));
-        s2 = sbox<D>(add(s2, ter[3 * r + 2]));
-        ext_layer(s0, s1, s2);
+        s0 = sbox_t<D>(add(s0, ter[3 * r + 0]));
+        s1 = sbox_t<D>(add(s1, ter[3 * r + 1]));
+        s2 = sbox_t<D>(add(s2, ter[3 * r + 2]));
+        ext_layer_t(s0, s1, s2);
     }
 }
 
@@ -238,6 +249,19 @@ __attribute__((target("avx512f,avx512ifma"))) void compress8_t(const Fr* left, c
     for (int k = 0; k < 5; ++k) s2.l[k] = _mm512_setzero_si512();
     permute<D>(s0, s1, s2, rc, L.rounds_f, L.rounds_p);
     store(s0, out, 1, n);
+}
+
+template <uint32_t D>
+__attribute__((target("avx512f,avx512ifma"))) void compress16_t(const Fr* left, const Fr* right, size_t stride,
+                                                                 Fr* out, int n, const V* rc, const P2Layout& L) {
+    const int n1 = n < 8 ? n : 8, n2 = n - n1;
+    W s0{load(left, stride, n1), load(left + 8 * stride, stride, n2)};
+    W s1{load(right, stride, n1), load(right + 8 * stride, stride, n2)};
+    W s2;
+    for (int k = 0; k < 5; ++k) s2.x.l[k] = s2.y.l[k] = _mm512_setzero_si512();
+    permute<D>(s0, s1, s2, rc, L.rounds_f, L.rounds_p);
+    store(s0.x, out, 1, n1);
+    store(s0.y, out + 8, 1, n2);
 }
 
 template <uint32_t D>
@@ -280,6 +304,14 @@ void compress8(const Fr* left, const Fr* right, size_t stride, Fr* out, int n, c
         compress8_t<17>(left, right, stride, out, n, rc_ptr(rc), L);
     else
         compress8_t<11>(left, right, stride, out, n, rc_ptr(rc), L);
+}
+
+void compress16(const Fr* left, const Fr* right, size_t stride, Fr* out, int n, const std::vector<Lane8>& rc,
+                const P2Layout& L) {
+    if (L.sbox_degree == 17)
+        compress16_t<17>(left, right, stride, out, n, rc_ptr(rc), L);
+    else
+        compress16_t<11>(left, right, stride, out, n, rc_ptr(rc), L);
 }
 
 void hash8(const Fr* rows, size_t w, Fr* out, int n, const std::vector<Lane8>& rc, const P2Layout& L) {

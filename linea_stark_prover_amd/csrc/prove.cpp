@@ -247,10 +247,12 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
         const size_t half = n / 2;
         if (half <= pool.size())  // one permutation per thread: the scalar path's latency is lower
             pool.parallel_for(half, [&](size_t i) { out[i] = ctx->p2.compress(in[2 * i], in[2 * i + 1]); });
-        else  // 8 at a time (AVX-512 IFMA when the CPU has it)
-            pool.parallel_for((half + 7) / 8, [&](size_t b) {
-                ctx->p2.compress_range(in, out, 8 * b, std::min(half, 8 * b + 8));
+        else {  // 8 or 16 at a time (AVX-512 IFMA when the CPU has it)
+            const size_t blk = half >= 16 * pool.size() ? 16 : 8;
+            pool.parallel_for((half + blk - 1) / blk, [&](size_t b) {
+                ctx->p2.compress_range(in, out, blk * b, std::min(half, blk * b + blk));
             });
+        }
         if (lo == 0) tt2 = clk::now();
         lo = end;
         end += n / 2;

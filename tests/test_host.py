@@ -122,7 +122,7 @@ def _host_merkle_checks(product_lib, ctx, pp, seed):
     """lsp_host_compress_batch / lsp_host_hash_rows (the tree-top path) vs the oracle"""
     from linea_stark_prover_amd.field import from_mont, to_mont
     rng = np.random.default_rng(seed)
-    for n in (1, 7, 8, 9, 37):
+    for n in (1, 7, 8, 9, 16, 17, 24, 37):
         vals = [int.from_bytes(rng.bytes(32), "little") % O.P for _ in range(2 * n)]
         pairs, out = to_mont(vals), np.zeros((n, 4), np.uint64)
         assert product_lib.lsp_host_compress_batch(ctx.h, ctypes.c_void_p(pairs.ctypes.data), n,

@@ -74,6 +74,19 @@ int bench_ifma() {
     for (int i = 0; i < N; ++i) { in[0] = p.compress(in[0], in[1]); }
     double us1 = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count() / N;
     printf("host compression: scalar %.2f us each; IFMA %.2f us per 8 (%.2f us each), mismatches %d\n", us1, us8, us8 / 8, bad);
+    // 16 lanes (two states in lockstep), every count 1..16
+    Fr in2[32], o16[16], r16[16];
+    for (auto& x : in2) x = rnd(g);
+    for (int n = 1; n <= 16; ++n) {
+        for (auto& x : o16) x = fr_zero();
+        p.compress_range(in2, r16, 0, n);
+        ifma::compress16(in2, in2 + 1, 2, o16, n, rc8, L);
+        for (int j = 0; j < n; ++j) bad += !fr_eq(o16[j], r16[j]);
+    }
+    t = std::chrono::steady_clock::now();
+    for (int i = 0; i < N; ++i) { ifma::compress16(in2, in2 + 1, 2, o16, 16, rc8, L); in2[0] = o16[3]; }
+    double us16 = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count() / N;
+    printf("IFMA x16: %.2f us per 16 (%.2f us each), mismatches %d\n", us16, us16 / 16, bad);
     return bad;
 }
 #endif

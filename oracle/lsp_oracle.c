@@ -494,6 +494,77 @@ void lo_coset_lde_batch(const lo_fr *in, size_t h, size_t w, uint32_t added_bits
     for (int t = 0; t < used; ++t) pthread_join(th[t], NULL);
 }
 
+/* ------------------------------------------------------ point evaluation */
+/* Barycentric evaluation of the columns given on H_h, independent of any NTT:
+ * p(x) = (x^h - 1)/h * sum_i y_i w^i / (x - w^i).  The full-size LDE checks
+ * (tests/test_gpu_fullsize.py) use it where the oracle's own LDE would take
+ * minutes.  Work is split into blocks of rows; each block inverts its own
+ * denominators and keeps a partial sum per column. */
+typedef struct {
+    const lo_fr *in; size_t h, w, nblk; lo_fr x, wh; lo_fr *part;
+} ev_ctx;
+static void ev_blocks(void *c, size_t lo, size_t hi) {
+    ev_ctx *E = (ev_ctx *)c;
+    for (size_t b = lo; b < hi; ++b) {
+        size_t r0 = b * E->h / E->nblk, r1 = (b + 1) * E->h / E->nblk, n = r1 - r0;
+        lo_fr *wi = (lo_fr *)malloc(n * sizeof(lo_fr)), *den = (lo_fr *)malloc(n * sizeof(lo_fr));
+        lo_fr *inv = (lo_fr *)malloc(n * sizeof(lo_fr));
+        lo_fr cur;
+        fpow64(&E->wh, r0, &cur);
+        for (size_t i = 0; i < n; ++i) {
+            wi[i] = cur;
+            fsub(&E->x, &cur, &den[i]);
+            fmul(&cur, &E->wh, &cur);
+        }
+        binv_ctx bc = {den, inv};
+        binv_range(&bc, 0, n);
+        lo_fr *acc = E->part + b * E->w;
+        for (size_t c2 = 0; c2 < E->w; ++c2) acc[c2] = ZERO_FR;
+        for (size_t i = 0; i < n; ++i) {
+            lo_fr f, t;
+            fmul(&wi[i], &inv[i], &f);
+            for (size_t c2 = 0; c2 < E->w; ++c2) {
+                fmul(&E->in[(r0 + i) * E->w + c2], &f, &t);
+                fadd(&acc[c2], &t, &acc[c2]);
+            }
+        }
+        free(wi);
+        free(den);
+        free(inv);
+    }
+}
+
+void lo_eval_points(const lo_fr *in, size_t h, size_t w, const lo_fr *xs, size_t npts, lo_fr *out, int nthreads) {
+    field_init();
+    size_t nblk = h < 256 ? h : 256;
+    lo_fr *part = (lo_fr *)malloc(nblk * w * sizeof(lo_fr));
+    lo_fr hinv, hf = fu(h);
+    finv(&hf, &hinv);
+    for (size_t k = 0; k < npts; ++k) {
+        ev_ctx E = {in, h, w, nblk, xs[k], two_adic_gen(log2_strict(h)), part};
+        parallel_for(nblk, nthreads, ev_blocks, &E);
+        lo_fr scale; /* (x^h - 1) / h */
+        fpow64(&xs[k], h, &scale);
+        fsub(&scale, &ONE, &scale);
+        fmul(&scale, &hinv, &scale);
+        for (size_t c2 = 0; c2 < w; ++c2) {
+            lo_fr s = ZERO_FR;
+            for (size_t b = 0; b < nblk; ++b) fadd(&s, &part[b * w + c2], &s);
+            fmul(&s, &scale, &out[k * w + c2]);
+        }
+    }
+    free(part);
+}
+
+/* x_j of LDE output row j (bit-reversed order over N = h << added_bits) */
+void lo_lde_point(size_t h, uint32_t added_bits, const lo_fr *shift, uint64_t j, lo_fr *out) {
+    field_init();
+    uint32_t lgN = log2_strict(h) + added_bits;
+    lo_fr wN = two_adic_gen(lgN);
+    fpow64(&wN, bitrev64(j, lgN), out);
+    fmul(out, shift, out);
+}
+
 /* -------------------------------------------------------------------- AIR */
 #define MAXC 256
 #define MAXT 32

@@ -53,6 +53,11 @@ void lo_poseidon2_permute(const lo_params *p, lo_fr state[3]);
 void lo_hash_iter(const lo_params *p, const lo_fr *in, size_t n, lo_fr *out);
 void lo_coset_lde_batch(const lo_fr *in, size_t h, size_t w, uint32_t added_bits,
                         const lo_fr *shifts /* w entries */, lo_fr *out, int nthreads);
+/* p_c(xs[k]) for the columns of a row-major h x w matrix of values on H_h
+ * (barycentric; no NTT); out is npts x w.  lo_lde_point: the point of LDE
+ * output row j (bit-reversed over N = h << added_bits, coset `shift`). */
+void lo_eval_points(const lo_fr *in, size_t h, size_t w, const lo_fr *xs, size_t npts, lo_fr *out, int nthreads);
+void lo_lde_point(size_t h, uint32_t added_bits, const lo_fr *shift, uint64_t j, lo_fr *out);
 /* Merkle over k equal-height matrices given as one row-major h x W buffer
  * (W = sum of widths, rows concatenated in commit order). layers_out gets
  * 2h-1 digests: leaves first, root last. */

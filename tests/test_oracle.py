@@ -206,3 +206,27 @@ def test_permutation_counts_match_survey_formula():
     expect = N * ((w + 1) // 2) + (N - 1) + N * ((q + 1) // 2) + (N - 1) + fri
     # + transcript hashes (a handful)
     assert expect <= O.PERM_COUNTER[0] <= expect + 200
+
+
+@pytest.mark.parametrize("logh,w,added", [(1, 1, 1), (4, 3, 3), (9, 2, 3)])
+def test_eval_points_matches_lde(oracle_lib, logh, w, added):
+    """lo_eval_points (barycentric, the full-size LDE spot check) and
+    lo_lde_point agree with the oracle's NTT-based coset LDE on every row."""
+    import ctypes
+    import numpy as np
+    L = oracle_lib.lib()
+    rng = np.random.default_rng(logh)
+    h, N = 1 << logh, 1 << (logh + added)
+    mat = rng.integers(0, 2**63, size=(h, w, 4), dtype=np.uint64)
+    mat[..., 3] &= (1 << 59) - 1  # < r (Montgomery words are any value < r)
+    shift = np.array([22, 0, 0, 0], np.uint64)
+    shifts = np.repeat(shift.reshape(1, 4), w, axis=0).copy()
+    lde = np.zeros((N, w, 4), np.uint64)
+    P = lambda a: ctypes.c_void_p(a.ctypes.data)
+    L.lo_coset_lde_batch(P(mat), ctypes.c_size_t(h), ctypes.c_size_t(w), added, P(shifts), P(lde), 4)
+    xs = np.zeros((N, 4), np.uint64)
+    for j in range(N):
+        L.lo_lde_point(ctypes.c_size_t(h), added, P(shift), ctypes.c_uint64(j), P(xs[j]))
+    got = np.zeros((N, w, 4), np.uint64)
+    L.lo_eval_points(P(mat), ctypes.c_size_t(h), ctypes.c_size_t(w), P(xs), ctypes.c_size_t(N), P(got), 4)
+    assert np.array_equal(got, lde)

@@ -102,3 +102,22 @@ def test_full_size_lde_tree_and_proof(gpu_ctx, oracle_lib, log_n):
             assert np.array_equal(cur[j], _oracle_compress(L, p, below[2 * j], below[2 * j + 1])), (lev, j)
         below = cur
     assert np.array_equal(below[0], root.reshape(4))
+
+
+def test_full_size_wide_air(gpu_ctx):
+    """configs[2]'s shape at its size: the C3 wide AIR (W = 184, 4 LogUp lookups
+    + 8 permutation groups) at 2^20 rows. Bit-exact parity for this AIR is in
+    tests/test_gpu_wide.py up to 2^12; here the proof must be deterministic,
+    verify, and fail once a quotient-root byte or an opened value is flipped."""
+    from linea_stark_prover_amd.prover import gen_wide_trace
+    a, d, _ = gpu_ctx.config.seeded()
+    trace, air = gen_wide_trace(20, a, d)
+    assert trace.shape[1] == 184
+    pub = np.concatenate([a, d])
+    proof = gpu_ctx.prove(trace, air, pub)
+    assert gpu_ctx.prove(trace, air, pub) == proof
+    assert gpu_ctx.verify(proof, air, pub)
+    for off in (60 + 8, 92 + 5 * 32 + 3):  # quotient root; an opened trace value at zeta
+        bad = bytearray(proof)
+        bad[off] ^= 1
+        assert not gpu_ctx.verify(bytes(bad), air, pub)

@@ -271,6 +271,8 @@ struct lsp_ctx {
     std::vector<hipEvent_t> event_pool;               // phase-timer events, reused across proofs
     std::map<std::pair<uint32_t, int>, uint4*> twiddles;
     std::map<std::string, const lsp::Fr*> ptabs;  // cached power tables (prove.cpp pow_table), pool-owned
+    std::map<uint32_t, std::vector<lsp::Fr>> fold_tw;  // host FRI fold factors g^-bitrev(i) per log2 length (prove.cpp)
+    size_t fri_host_tail = 2048;  // FRI rounds of at most this many leaves run wholly on the host (prove.cpp)
     std::vector<std::pair<std::string, double>> timings;
 
     void* buf(const std::string& name, size_t bytes);

@@ -179,6 +179,33 @@ struct TopTimes {
 };
 static TopTimes g_top_times;
 
+// The levels above `first` digests host[0, first): each level compresses
+// pairs with the host pool and is appended; returns the end of the layers
+// (the root is host[end - 1]).  *t_first (if given) is set after the first level.
+static size_t host_levels(lsp_ctx* ctx, Fr* host, size_t first,
+                          std::chrono::steady_clock::time_point* t_first = nullptr) {
+    HostPool& pool = ctx->host_pool();
+    size_t lo = 0, n = first, end = first;
+    while (n > 1) {
+        Fr* out = host + end;
+        const Fr* in = host + lo;
+        const size_t half = n / 2;
+        if (half <= pool.size())  // one permutation per thread: the scalar path's latency is lower
+            pool.parallel_for(half, [&](size_t i) { out[i] = ctx->p2.compress(in[2 * i], in[2 * i + 1]); });
+        else {  // 8 or 16 at a time (AVX-512 IFMA when the CPU has it)
+            const size_t blk = half >= 16 * pool.size() ? 16 : 8;
+            pool.parallel_for((half + blk - 1) / blk, [&](size_t b) {
+                ctx->p2.compress_range(in, out, blk * b, std::min(half, blk * b + blk));
+            });
+        }
+        if (lo == 0 && t_first) *t_first = std::chrono::steady_clock::now();
+        lo = end;
+        end += n / 2;
+        n /= 2;
+    }
+    return end;
+}
+
 Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, const FoldSpec* fold) {
     hipStream_t st = ctx->stream;
     using clk = std::chrono::steady_clock;
@@ -240,24 +267,7 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
     const auto tt1 = clk::now();
     auto tt2 = tt1;
     const size_t first = len;  // the part already on the device (unless hashed here)
-    size_t lo = 0, n = first, end = first;
-    while (n > 1) {
-        Fr* out = host + end;
-        const Fr* in = host + lo;
-        const size_t half = n / 2;
-        if (half <= pool.size())  // one permutation per thread: the scalar path's latency is lower
-            pool.parallel_for(half, [&](size_t i) { out[i] = ctx->p2.compress(in[2 * i], in[2 * i + 1]); });
-        else {  // 8 or 16 at a time (AVX-512 IFMA when the CPU has it)
-            const size_t blk = half >= 16 * pool.size() ? 16 : 8;
-            pool.parallel_for((half + blk - 1) / blk, [&](size_t b) {
-                ctx->p2.compress_range(in, out, blk * b, std::min(half, blk * b + blk));
-            });
-        }
-        if (lo == 0) tt2 = clk::now();
-        lo = end;
-        end += n / 2;
-        n /= 2;
-    }
+    const size_t end = host_levels(ctx, host, first, &tt2);
     if (g_top_times.on) {
         const auto tt3 = clk::now();
         g_top_times.n++;
@@ -615,10 +625,77 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                                     pend.vout, st, pend.i0, (int)pend.logm));
             pending = false;
         };
+        size_t host_tail = ctx->fri_host_tail;
+        if (const char* e = std::getenv("LSP_FRI_HOST_TAIL")) host_tail = std::strtoull(e, nullptr, 10);
+        const Fr* hfin = nullptr;  // the final vector, when the host ran the last rounds
         while (len > final_len) {
             if (sharded && (len >> b) < 2 * FRI_SHARD_MIN) {
                 flush_fold();  // the gathered vector must exist
                 replicate();
+            }
+            if (!sharded && len / 2 <= host_tail) {
+                // The last rounds wholly on the host: their trees are a few thousand
+                // permutations in a chain of short levels (~58 us each on the GPU, a few
+                // us on the host pool).  One download of the vector; per round the host
+                // hashes the tree, samples beta and folds; the layers and folded vectors
+                // go back asynchronously for the query openings, which gather on the device.
+                flush_fold();
+                size_t hn = final_len, ht = 0;
+                for (size_t l = len; l > final_len; l /= 2) {
+                    hn += l;
+                    ht += l - 1;
+                }
+                Fr* hv = (Fr*)ctx->hbuf("fri_tail", (hn + ht) * sizeof(Fr));
+                Fr* htr = hv + hn;
+                LSP_HIP(hipMemcpyAsync(hv, fv + vo, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
+                LSP_HIP(hipStreamSynchronize(st));
+                HostPool& pool = ctx->host_pool();
+                size_t hvo = 0, hto = 0;
+                while (len > final_len) {
+                    const size_t m = len / 2;
+                    const uint32_t logm = log2_exact(m);
+                    const Fr* v = hv + hvo;
+                    Fr* lay = htr + hto;
+                    pool.parallel_for((m + 7) / 8, [&](size_t blk) {
+                        ctx->p2.hash_range(v, 2, lay, 8 * blk, std::min(m, 8 * blk + 8));
+                    });
+                    const size_t end = host_levels(ctx, lay, m);
+                    LSP_HIP(hipMemcpyAsync(ftree + to, lay, end * sizeof(Fr), hipMemcpyHostToDevice, st));
+                    FriRound R;
+                    R.vec = fv + vo;
+                    R.tree = ftree + to;
+                    R.ml = m;
+                    R.sharded = false;
+                    const Fr root = lay[end - 1];
+                    proof->roots.push_back(root);
+                    ch.observe(root);
+                    const Fr hb = fr_mul(ch.sample(), half);
+                    std::vector<Fr>& tw = ctx->fold_tw[logm];  // g^-bitrev(i), g = w_{2m}
+                    if (tw.size() != m) {
+                        const Fr ginv = host_inv_cached(host_two_adic_generator(logm + 1));
+                        std::vector<Fr> pw(m);
+                        pw[0] = one;
+                        for (size_t j = 1; j < m; ++j) pw[j] = fr_mul(pw[j - 1], ginv);
+                        tw.resize(m);
+                        for (size_t i = 0; i < m; ++i) tw[i] = pw[host_bitrev(i, logm)];
+                    }
+                    Fr* out = hv + hvo + len;
+                    pool.parallel_for((m + 63) / 64, [&](size_t blk) {
+                        for (size_t i = 64 * blk; i < std::min(m, 64 * blk + 64); ++i) {
+                            const Fr p = fr_mul(hb, tw[i]);
+                            out[i] = fr_add(fr_mul(fr_add(half, p), v[2 * i]), fr_mul(fr_sub(half, p), v[2 * i + 1]));
+                        }
+                    });
+                    LSP_HIP(hipMemcpyAsync(fv + vo + len, out, m * sizeof(Fr), hipMemcpyHostToDevice, st));
+                    rounds.push_back(std::move(R));
+                    hvo += len;
+                    vo += len;
+                    hto += end;
+                    to += end;
+                    len = m;
+                }
+                hfin = hv + hvo;
+                break;
             }
             const size_t m = len / 2, ml = sharded ? (m >> b) : m;
             FriRound R;
@@ -654,7 +731,9 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         flush_fold();
         if (sharded) replicate();
         std::vector<Fr> fin(len);
-        {
+        if (hfin)
+            std::copy(hfin, hfin + len, fin.begin());
+        else {
             Fr* hf = (Fr*)ctx->hbuf("f_final_h", len * sizeof(Fr));
             LSP_HIP(hipMemcpyAsync(hf, fv + vo, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
             LSP_HIP(hipStreamSynchronize(st));

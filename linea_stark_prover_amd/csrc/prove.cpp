@@ -179,25 +179,27 @@ struct TopTimes {
 };
 static TopTimes g_top_times;
 
+// out[i] = compress(in[2i], in[2i+1]) for i < half on the host pool
+static void host_compress_level(lsp_ctx* ctx, const Fr* in, Fr* out, size_t half) {
+    HostPool& pool = ctx->host_pool();
+    if (half <= pool.size())  // one permutation per thread: the scalar path's latency is lower
+        pool.parallel_for(half, [&](size_t i) { out[i] = ctx->p2.compress(in[2 * i], in[2 * i + 1]); });
+    else {  // 8 or 16 at a time (AVX-512 IFMA when the CPU has it)
+        const size_t blk = half >= 16 * pool.size() ? 16 : 8;
+        pool.parallel_for((half + blk - 1) / blk, [&](size_t b) {
+            ctx->p2.compress_range(in, out, blk * b, std::min(half, blk * b + blk));
+        });
+    }
+}
+
 // The levels above `first` digests host[0, first): each level compresses
 // pairs with the host pool and is appended; returns the end of the layers
 // (the root is host[end - 1]).  *t_first (if given) is set after the first level.
 static size_t host_levels(lsp_ctx* ctx, Fr* host, size_t first,
                           std::chrono::steady_clock::time_point* t_first = nullptr) {
-    HostPool& pool = ctx->host_pool();
     size_t lo = 0, n = first, end = first;
     while (n > 1) {
-        Fr* out = host + end;
-        const Fr* in = host + lo;
-        const size_t half = n / 2;
-        if (half <= pool.size())  // one permutation per thread: the scalar path's latency is lower
-            pool.parallel_for(half, [&](size_t i) { out[i] = ctx->p2.compress(in[2 * i], in[2 * i + 1]); });
-        else {  // 8 or 16 at a time (AVX-512 IFMA when the CPU has it)
-            const size_t blk = half >= 16 * pool.size() ? 16 : 8;
-            pool.parallel_for((half + blk - 1) / blk, [&](size_t b) {
-                ctx->p2.compress_range(in, out, blk * b, std::min(half, blk * b + blk));
-            });
-        }
+        host_compress_level(ctx, host + lo, host + end, n / 2);
         if (lo == 0 && t_first) *t_first = std::chrono::steady_clock::now();
         lo = end;
         end += n / 2;
@@ -640,6 +642,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                 // hashes the tree, samples beta and folds; the layers and folded vectors
                 // go back asynchronously for the query openings, which gather on the device.
                 flush_fold();
+                const auto th0 = std::chrono::steady_clock::now();
                 size_t hn = final_len, ht = 0;
                 for (size_t l = len; l > final_len; l /= 2) {
                     hn += l;
@@ -649,6 +652,8 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                 Fr* htr = hv + hn;
                 LSP_HIP(hipMemcpyAsync(hv, fv + vo, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
                 LSP_HIP(hipStreamSynchronize(st));
+                const auto th1 = std::chrono::steady_clock::now();
+                const size_t rounds_gpu = rounds.size();
                 HostPool& pool = ctx->host_pool();
                 size_t hvo = 0, hto = 0;
                 while (len > final_len) {
@@ -656,9 +661,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                     const uint32_t logm = log2_exact(m);
                     const Fr* v = hv + hvo;
                     Fr* lay = htr + hto;
-                    pool.parallel_for((m + 7) / 8, [&](size_t blk) {
-                        ctx->p2.hash_range(v, 2, lay, 8 * blk, std::min(m, 8 * blk + 8));
-                    });
+                    host_compress_level(ctx, v, lay, m);  // a 2-element leaf's hash_iter is compress (A4/A5)
                     const size_t end = host_levels(ctx, lay, m);
                     LSP_HIP(hipMemcpyAsync(ftree + to, lay, end * sizeof(Fr), hipMemcpyHostToDevice, st));
                     FriRound R;
@@ -695,6 +698,11 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                     len = m;
                 }
                 hfin = hv + hvo;
+                if (g_top_times.on)
+                    std::fprintf(stderr, "[fri tail] %zu rounds on the host: %.1f us (download %.1f us)\n",
+                                 rounds.size() - rounds_gpu,
+                                 std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - th0).count(),
+                                 std::chrono::duration<double, std::micro>(th1 - th0).count());
                 break;
             }
             const size_t m = len / 2, ml = sharded ? (m >> b) : m;

@@ -1,6 +1,6 @@
 """Parity at BASELINE.json's full sizes: the bench workload (3x3 permutation
 AIR, 2^19 rows) and configs[1] (2^22 rows).  The whole oracle prover takes
-minutes there, so these tests check the trace commitment in full and the rest
+minutes there at 2^22, so these tests check the trace commitment in full and the rest
 through properties that hold at any size (box timings: 18 s and 35 s):
 
 * the trace LDE: every value against the C oracle's NTT LDE (bit-exact), and
@@ -11,7 +11,8 @@ through properties that hold at any size (box timings: 18 s and 35 s):
   tree (root and leaves); at both sizes sampled leaves against the oracle's
   sponge, sampled nodes of every level against the oracle's compression, and
   the root against the trace root inside the fused `lsp_prove` proof;
-* the proof: deterministic, accepted by the verifier, rejected once tampered.
+* the proof: deterministic, accepted by the verifier, rejected once tampered;
+* at 2^19 the whole proof byte for byte against the oracle's proof (36 s).
 """
 import ctypes
 
@@ -121,3 +122,22 @@ def test_full_size_wide_air(gpu_ctx):
         bad = bytearray(proof)
         bad[off] ^= 1
         assert not gpu_ctx.verify(bytes(bad), air, pub)
+
+
+def test_full_proof_bench_size_vs_oracle(gpu_ctx, oracle_lib):
+    """The whole 2^19-row proof (the bench workload) byte for byte against the C
+    oracle's proof of the same trace (~36 s of oracle time on 16 host threads;
+    2^22 was run the same way, `tools/full_oracle_proof.py`,
+    `profiles/r01q_full_oracle_proofs.txt`)."""
+    import os
+
+    from linea_stark_prover_amd.air import permutation_air
+    log_n = 19
+    p = oracle_lib.setup()
+    tb, w = oracle_lib.gen_perm_trace(p, log_n, 3)
+    trace = np.frombuffer(tb, dtype=np.uint64).reshape(1 << log_n, w, 4).copy()
+    pub = np.concatenate([np.array(p.alpha, np.uint64).reshape(1, 4), np.array(p.delta, np.uint64).reshape(1, 4)])
+    proof = gpu_ctx.prove(trace, permutation_air(3), pub)
+    threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share (os.cpu_count() shows the whole machine)
+    expect = oracle_lib.prove(p, tb, 1 << log_n, w, oracle_lib.perm_air(3), nthreads=threads)
+    assert proof == expect

@@ -4,7 +4,8 @@ against the C oracle's proof of the same seeded trace, byte for byte.
 The oracle (oracle/lsp_oracle.c, test infrastructure) is only the checker; it
 takes minutes at 2^22 on 16 host threads, which is why this is a tool run
 recorded under profiles/ and not part of the GPU test suite.
-Usage: python tools/full_oracle_proof.py LOG_N [LOG_N ...]   (threads: LSP_ORACLE_THREADS, default 16)"""
+Usage: python tools/full_oracle_proof.py LOG_N[xNCOLS] ...   (e.g. 19 22 19x6; NCOLS 3 by default;
+       threads: LSP_ORACLE_THREADS, default 16)"""
 import hashlib
 import os
 import sys
@@ -18,7 +19,6 @@ from linea_stark_prover_amd.air import permutation_air  # noqa: E402
 from linea_stark_prover_amd.prover import Context, StarkConfig  # noqa: E402
 from oracle import cref  # noqa: E402
 
-ncols = 3
 nthreads = int(os.environ.get("LSP_ORACLE_THREADS", "16"))
 p = cref.setup()
 pub = np.concatenate([np.array(p.alpha, np.uint64).reshape(1, 4), np.array(p.delta, np.uint64).reshape(1, 4)])
@@ -32,7 +32,9 @@ def heartbeat(stop):  # a line a minute while the oracle runs (long silent runs 
 
 
 with Context(StarkConfig(), device=0) as ctx:
-    for log_n in [int(x) for x in sys.argv[1:] or ["19"]]:
+    for arg in sys.argv[1:] or ["19"]:
+        log_n, _, nc = arg.partition("x")
+        log_n, ncols = int(log_n), int(nc or 3)
         t0 = time.time()
         tb, w = cref.gen_perm_trace(p, log_n, ncols)
         trace = np.frombuffer(tb.raw, dtype=np.uint64).reshape(1 << log_n, w, 4)
@@ -47,7 +49,7 @@ with Context(StarkConfig(), device=0) as ctx:
         same = gpu == ref
         ok_all &= same
         verified = ctx.verify(gpu, permutation_air(ncols), pub)
-        print(f"log_n={log_n} w={w}: trace {t1 - t0:.1f} s; GPU proof {t2 - t1:.2f} s (incl. upload, first call); "
+        print(f"log_n={log_n} {ncols}x{ncols} AIR w={w}: trace {t1 - t0:.1f} s; GPU proof {t2 - t1:.2f} s (incl. upload, first call); "
               f"oracle proof {t3 - t2:.1f} s on {nthreads} threads; {len(gpu)} bytes; "
               f"sha256 {hashlib.sha256(gpu).hexdigest()[:16]} / {hashlib.sha256(ref).hexdigest()[:16]}; "
               f"byte-identical={same}; verified={verified}", flush=True)

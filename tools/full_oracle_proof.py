@@ -4,7 +4,8 @@ against the C oracle's proof of the same seeded trace, byte for byte.
 The oracle (oracle/lsp_oracle.c, test infrastructure) is only the checker; it
 takes minutes at 2^22 on 16 host threads, which is why this is a tool run
 recorded under profiles/ and not part of the GPU test suite.
-Usage: python tools/full_oracle_proof.py LOG_N[xNCOLS] ...   (e.g. 19 22 19x6; NCOLS 3 by default;
+Usage: python tools/full_oracle_proof.py LOG_N[xNCOLS] | wLOG_N ...   (e.g. 19 22 19x6 w20; NCOLS 3 by default;
+       wLOG_N: the wide C3 AIR, 4 LogUp lookups + 8 groups of 6+6, W = 184;
        threads: LSP_ORACLE_THREADS, default 16)"""
 import hashlib
 import os
@@ -33,6 +34,29 @@ def heartbeat(stop):  # a line a minute while the oracle runs (long silent runs 
 
 with Context(StarkConfig(), device=0) as ctx:
     for arg in sys.argv[1:] or ["19"]:
+        if arg.startswith("w"):  # the wide AIR
+            from linea_stark_prover_amd.prover import gen_wide_trace
+            log_n = int(arg[1:])
+            a, d, _ = ctx.config.seeded()
+            t0 = time.time()
+            tr, air = gen_wide_trace(log_n, a, d)
+            t1 = time.time()
+            wpub = np.concatenate([a, d])
+            gpu = ctx.prove(tr, air, wpub)
+            t2 = time.time()
+            stop = threading.Event()
+            threading.Thread(target=heartbeat, args=(stop,), daemon=True).start()
+            ref = cref.prove(p, tr.ctypes.data, 1 << log_n, tr.shape[1], air.descriptor(), nthreads=nthreads)
+            stop.set()
+            t3 = time.time()
+            same = gpu == ref
+            ok_all &= same
+            print(f"log_n={log_n} wide AIR w={tr.shape[1]}: trace {t1 - t0:.1f} s; GPU proof {t2 - t1:.2f} s (incl. upload, "
+                  f"first call); oracle proof {t3 - t2:.1f} s on {nthreads} threads; {len(gpu)} bytes; "
+                  f"sha256 {hashlib.sha256(gpu).hexdigest()[:16]} / {hashlib.sha256(ref).hexdigest()[:16]}; "
+                  f"byte-identical={same}; verified={ctx.verify(gpu, air, wpub)}", flush=True)
+            del tr
+            continue
         log_n, _, nc = arg.partition("x")
         log_n, ncols = int(log_n), int(nc or 3)
         t0 = time.time()

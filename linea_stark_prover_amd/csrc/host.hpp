@@ -251,7 +251,7 @@ struct lsp_ctx {
     int device = 0;
     lsp::Comm* comm = nullptr;  // attached communicator of a process-per-GPU sharded prove (owned)
     std::unique_ptr<lsp::HostPool> pool_;  // lazily created (host_pool())
-    size_t host_tree_top = 256;             // Merkle levels at or below this many digests run on the host (16 threads: ~30 us for the 256 -> 128 level vs ~55 us on the GPU)
+    size_t host_tree_top = 1024;            // Merkle levels at or below this many digests run on the host (16 threads, 16-lane IFMA: ~20 us for the 1024 -> 512 level vs ~58 us on the GPU; 1024 beat 256 by ~0.45 ms per 2^19 proof in interleaved same-box runs)
     hipStream_t stream = nullptr;
     lsp::P2Host p2;
     lsp::Fr* rc_dev = nullptr;    // round constants, ark form

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -179,6 +180,18 @@ struct TopTimes {
 };
 static TopTimes g_top_times;
 
+// Proofs running at once in this process (several contexts in flight, or the
+// ranks of an in-process group).  A lone proof hands its trees to the host
+// pool from host_tree_top digests; concurrent proofs share the host's cores,
+// so there the host takes over only from 256 digests (bench, same box:
+// 1024 vs 256 = 67.6 vs 68.3 ms alone, 62.3 vs 60.0 ms per proof with three in flight).
+static std::atomic<int> g_active_proofs{0};
+struct ActiveProof {
+    ActiveProof() { g_active_proofs.fetch_add(1, std::memory_order_relaxed); }
+    ~ActiveProof() { g_active_proofs.fetch_sub(1, std::memory_order_relaxed); }
+};
+constexpr size_t SHARED_HOST_TREE_TOP = 256;
+
 // out[i] = compress(in[2i], in[2i+1]) for i < half on the host pool
 static void host_compress_level(lsp_ctx* ctx, const Fr* in, Fr* out, size_t half) {
     HostPool& pool = ctx->host_pool();
@@ -213,6 +226,7 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
     using clk = std::chrono::steady_clock;
     const auto tt0 = clk::now();
     size_t top = ctx->host_tree_top;
+    if (g_active_proofs.load(std::memory_order_relaxed) > 1) top = std::min(top, SHARED_HOST_TREE_TOP);
     if (const char* e = std::getenv("LSP_HOST_TREE_TOP")) top = std::strtoull(e, nullptr, 10);
     HostPool& pool = ctx->host_pool();
     size_t off = 0, len = height;
@@ -372,6 +386,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                        const Fr* pub, size_t npub) {
     LSP_REQUIRE(npub >= 2, LSP_E_ARG, "public values must hold [alpha, delta]");
     LSP_REQUIRE(air.max_col < w, LSP_E_ARG, "AIR column id outside the trace width");
+    const ActiveProof active;
     const uint32_t log_h = log2_exact(h);
     LSP_REQUIRE(h >= 2, LSP_E_SIZE, "trace needs at least 2 rows");
     const uint32_t lb = ctx->log_blowup;

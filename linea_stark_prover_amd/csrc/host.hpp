@@ -271,6 +271,16 @@ struct lsp_ctx {
     std::vector<hipEvent_t> event_pool;               // phase-timer events, reused across proofs
     std::map<std::pair<uint32_t, int>, uint4*> twiddles;
     std::map<std::string, const lsp::Fr*> ptabs;  // cached power tables (prove.cpp pow_table), pool-owned
+    // Inside lsp_prove the host-made tree-top layers are only read by the query
+    // gather at the end, so their uploads wait there instead of delaying the next
+    // kernel on the stream (prove.cpp commit_device / flush_top_uploads).
+    struct TopUpload {
+        void* dst;
+        const void* src;
+        size_t bytes;
+    };
+    bool defer_top_uploads = false;
+    std::vector<TopUpload> top_uploads;
     std::map<uint32_t, std::vector<lsp::Fr>> fold_tw;  // host FRI fold factors g^-bitrev(i) per log2 length (prove.cpp)
     size_t fri_host_tail = 2048;  // FRI rounds of at most this many leaves run wholly on the host (prove.cpp)
     std::vector<std::pair<std::string, double>> timings;

@@ -221,6 +221,32 @@ static size_t host_levels(lsp_ctx* ctx, Fr* host, size_t first,
     return end;
 }
 
+// the pinned buffer of a tree's host layers: one per tree while uploads are
+// deferred (each must stay intact until flush_top_uploads), else one shared
+static std::string top_buf_name(lsp_ctx* ctx) {
+    return ctx->defer_top_uploads ? "merkle_top" + std::to_string(ctx->top_uploads.size()) : std::string("merkle_top");
+}
+
+// issue the deferred tree-top uploads on the context's stream
+static void flush_top_uploads(lsp_ctx* ctx) {
+    for (const auto& u : ctx->top_uploads)
+        LSP_HIP(hipMemcpyAsync(u.dst, u.src, u.bytes, hipMemcpyHostToDevice, ctx->stream));
+    ctx->top_uploads.clear();
+}
+
+// defers the uploads for one proof; the destructor drops any left (an error path)
+struct DeferTopUploads {
+    lsp_ctx* ctx;
+    explicit DeferTopUploads(lsp_ctx* c) : ctx(c) {
+        ctx->top_uploads.clear();
+        ctx->defer_top_uploads = std::getenv("LSP_NO_DEFER_TOPS") == nullptr;
+    }
+    ~DeferTopUploads() {
+        ctx->defer_top_uploads = false;
+        ctx->top_uploads.clear();
+    }
+};
+
 Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, const FoldSpec* fold) {
     hipStream_t st = ctx->stream;
     using clk = std::chrono::steady_clock;
@@ -240,7 +266,7 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
     Fr* host;  // host layers, starting at device offset `off` (pinned)
     if (leaves_on_host) {
         const size_t w = m.width[0];
-        host = (Fr*)ctx->hbuf("merkle_top", (2 * height - 1 + height * w) * sizeof(Fr));
+        host = (Fr*)ctx->hbuf(top_buf_name(ctx), (2 * height - 1 + height * w) * sizeof(Fr));
         Fr* rows = host + 2 * height - 1;
         LSP_HIP(hipMemcpyAsync(rows, m.ptr[0], height * w * sizeof(Fr), hipMemcpyDeviceToHost, st));
         LSP_HIP(hipStreamSynchronize(st));
@@ -266,7 +292,7 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
         LSP_HIP(hipEventRecord(ctx->ev_near, st));
         LSP_HIP(launch_merkle_levels(layers + off1, len1, top, ctx->rc29_dev, ctx->p2.L, &off, &len, st));
         off += off1;
-        host = (Fr*)ctx->hbuf("merkle_top", (2 * len - 1) * sizeof(Fr));
+        host = (Fr*)ctx->hbuf(top_buf_name(ctx), (2 * len - 1) * sizeof(Fr));
         LSP_HIP(hipMemcpyAsync(host, layers + off, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
         LSP_HIP(hipEventRecord(ctx->ev_top, st));
         // sleep through the wide levels, then spin (with the pool awake) for the last ones
@@ -292,8 +318,12 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
         g_top_times.first_us += std::chrono::duration<double, std::micro>(tt2 - tt1).count();
     }
     const size_t skip = leaves_on_host ? 0 : first;  // host-made digests start here
-    if (end > skip)
-        LSP_HIP(hipMemcpyAsync(layers + off + skip, host + skip, (end - skip) * sizeof(Fr), hipMemcpyHostToDevice, st));
+    if (end > skip) {
+        if (ctx->defer_top_uploads)
+            ctx->top_uploads.push_back({layers + off + skip, host + skip, (end - skip) * sizeof(Fr)});
+        else
+            LSP_HIP(hipMemcpyAsync(layers + off + skip, host + skip, (end - skip) * sizeof(Fr), hipMemcpyHostToDevice, st));
+    }
     return host[end - 1];
 }
 
@@ -387,6 +417,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
     LSP_REQUIRE(npub >= 2, LSP_E_ARG, "public values must hold [alpha, delta]");
     LSP_REQUIRE(air.max_col < w, LSP_E_ARG, "AIR column id outside the trace width");
     const ActiveProof active;
+    const DeferTopUploads defer(ctx);
     const uint32_t log_h = log2_exact(h);
     LSP_REQUIRE(h >= 2, LSP_E_SIZE, "trace needs at least 2 rows");
     const uint32_t lb = ctx->log_blowup;
@@ -794,6 +825,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         // ---- query phase: the owner of a query's row (rank idx / S) gathers the
         // openings below the rank subtrees in one kernel; the layers above come
         // from the host top trees every rank holds.
+        flush_top_uploads(ctx);  // the gather below reads the tree tops
         T.begin("query phase");
         const auto q0 = std::chrono::steady_clock::now();
         const uint32_t nr = (uint32_t)rounds.size();

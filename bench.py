@@ -6,33 +6,53 @@ A "step" is one full ``p3_uni_stark::prove`` (bin/src/main.rs:80-86) of the
 3x3 permutation AIR (3 'from' + 3 'to' columns + b_inverse + check, w = 8,
 4 quotient chunks, log_blowup 3, 33 queries) on one synthetic 2^log_n-row
 trace that is already resident in HBM, ending with the serialized proof on
-the host.  For N > 1 (launched by torch.distributed.run) every rank proves its
-own independent trace (SURVEY 8(d) C5, replicas, no data-path collective);
-``value`` = all rows proven by all ranks / the max-over-ranks wall time.
+the host.
 
-``--shard``: the N ranks prove ONE trace together
-(lsp_prove_sharded; rank g owns LDE rows [g N/G, (g+1) N/G)), exchanging
-subtree roots, quotient chunks, opened values and query openings over RCCL
-(``--comm rccl``, device-direct over xGMI) or a gloo group (``--comm gloo``,
-host-staged; lets several ranks share one GPU).  ``value`` = rows of the one
-proof / max-over-ranks wall time ("scaling": "strong").
+Ranks.  ``--gpus N`` with N > 1 needs N processes: under
+torch.distributed.run (WORLD_SIZE set) every process is one rank; started
+without a launcher, bench.py starts ``torch.distributed.run --nproc-per-node
+N`` itself as a child process (before anything touches the GPU) and exits with
+its status.  WORLD_SIZE != --gpus is an error, never a silent single rank.
 
-Besides the contract fields the JSON line carries:
+Legs (rank 0 prints ONE JSON line):
+  value          C5 replicas: every rank proves its own
+                 independent 2^log_n trace, no data-path collective; value =
+                 all rows / max-over-ranks wall time ("scaling": "weak").
+                 ``--shard`` instead proves ONE trace over the N ranks
+                 (lsp_prove_sharded, "scaling": "strong").
+  sharded        C4 (BASELINE configs[3]): one 2^24-row proof
+                 sharded over all N ranks (rank g owns LDE rows
+                 [g N/G, (g+1) N/G)), exchanging subtree roots, quotient
+                 chunks, opened values and query openings over RCCL (one GPU
+                 per rank) or gloo (ranks sharing a GPU); at N = 8 also
+                 2^26.  The trace is generated on every GPU from the same
+                 seed (lsp_gen_permutation_trace_device).  At N = 1 it is
+                 lsp_prove itself: prove_shard over the one-rank SoloComm.
+                 A per-rank watchdog bounds the leg (--shard-timeout).
+  prove_time_host_trace_s   (N = 1) the same proof with the trace uploaded
+                 from host memory inside every step (SURVEY 8(d) "H2D
+                 included"); mean and median.
   roofline       the coset LDE (the metric's "NTT HBM GB/s"): algorithmic
                  bytes 32*w*(h + N) per coset_lde_batch / its event-timed
                  duration, vs the 8 TB/s HBM3E peak
   roofline_valu  the dominant kernel family (Poseidon2 Merkle hashing):
-                 permutations / time vs the permutation rate of the same
-                 code on register-resident states (lsp_calibrate_poseidon2)
-  cpu_baseline   the C restatement (oracle/, "port") proving a bounded
-                 sample on the host cores, rank 0 at N = 1 only
+                 permutations / time vs the chip's peak permutation rate
+                 from the measured v_mad_u64_u32 issue rate
+                 (profiles/r02_rates.json, tools/ubench/rates.hip): 230
+                 Fr-muls x 128 MADs per permutation
+  cpu_baseline   the C restatement (oracle/, "port") proving the headline
+                 2^19 workload on the host cores, rank 0 at N = 1 only
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import statistics
+import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -41,9 +61,14 @@ sys.path.insert(0, ROOT)
 METRIC = "prove time (s) + trace-rows/sec, 3x3 perm AIR @2^19; NTT HBM GB/s vs roofline"
 PUBLISHED_ROWS_PER_S = 524288 / 330.0  # README.md:11 (~330 s for 2^19 rows, CPU)
 HBM_PEAK_GBS = 8000.0
+RATES_FILE = os.path.join(ROOT, "profiles", "r02_rates.json")
+NOMINAL_GHZ = 2.4           # MI355X peak engine clock (MI355X_MICROARCH.md)
+SIMDS = 256 * 4             # 256 CUs x 4 SIMD-32 units
+FR_MUL_PER_PERM = 230       # 46 S-boxes x 5 products (x^11), SURVEY 8 conventions
+MAD_PER_FR_MUL = 128        # 8 x 32-bit limbs: 64 product + 64 reduction MADs (the floor the peak assumes)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -55,34 +80,107 @@ def parse():
                          "wide AIR (4 LogUp lookups + 8 permutation groups of 6+6, W = 184)")
     ap.add_argument("--seed", type=int, default=0x4C494E4541)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-log-n", type=int, default=17, help="bounded CPU-baseline sample size")
-    ap.add_argument("--shard", action="store_true", help="one proof sharded over the N ranks (C4)")
+    ap.add_argument("--cpu-log-n", type=int, default=19, help="CPU-baseline sample size (rows = 2^cpu_log_n)")
+    ap.add_argument("--shard", action="store_true", help="main leg: one proof sharded over the N ranks (C4)")
     ap.add_argument("--comm", choices=["rccl", "gloo"], default="rccl", help="--shard exchange transport")
-    ap.add_argument("--device", type=int, default=None, help="GPU of this rank (default: LOCAL_RANK)")
+    ap.add_argument("--shard-leg", default="auto",
+                    help="C4 'sharded' leg sizes, comma-separated log2 rows; 'auto' = 24 (and 26 at N = 8); "
+                         "'none' disables")
+    ap.add_argument("--shard-leg-steps", type=int, default=2)
+    ap.add_argument("--shard-leg-warmup", type=int, default=1)
+    ap.add_argument("--shard-comm", choices=["auto", "rccl", "gloo"], default="auto",
+                    help="auto: RCCL when every rank has its own GPU, else gloo")
+    ap.add_argument("--shard-timeout", type=float, default=900.0,
+                    help="seconds before a rank's watchdog abandons the sharded leg")
+    ap.add_argument("--no-host-trace-leg", action="store_true")
+    ap.add_argument("--device", type=int, default=None, help="GPU of this rank (default: LOCAL_RANK mod #GPUs)")
     ap.add_argument("--dump-proof", default=None, help="rank 0 writes the last proof here")
     ap.add_argument("--inflight", type=int, default=3,
                     help="also measure P independent proofs in flight on the GPU (P contexts/streams, "
                          "reported as the separate 'inflight' field, never as value); 0 or 1 disables")
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="set up the ranks and the control group, print the rank census, no GPU work")
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: run N ranks under torch.distributed.run
+    as a child process (nothing here has touched the GPU) and return its status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
-    from linea_stark_prover_amd.replicas import init_from_env, rank_seed, timed_steps
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        print(json.dumps({"error": f"WORLD_SIZE={world_env} but --gpus {args.gpus}: refusing to report "
+                                   f"{world_env} rank(s) as {args.gpus} GPU(s)"}), flush=True)
+        return 2
+    from linea_stark_prover_amd.replicas import init_from_env
     dist = init_from_env()  # gloo control plane when WORLD_SIZE > 1 (imports torch first)
-    world, rank, local = dist.world, dist.rank, dist.local_rank
+    world, rank = dist.world, dist.rank
+    ranks_seen = int(round(dist.sum(1.0)))
+    if args.dry_run:
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "n_ranks_seen": ranks_seen,
+                              "launcher": "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ
+                              else "env"}), flush=True)
+        dist.close()
+        return 0
 
-    import numpy as np
+    shard_sizes = shard_leg_sizes(args, world)
+    if args.shard or (shard_sizes and world > 1):
+        from linea_stark_prover_amd import shard as S  # noqa: F401  (torch before the HIP library)
+    out, ctx = main_leg(args, dist, ranks_seen)
+    if shard_sizes:
+        sharded = guarded_shard_leg(args, dist, ctx, shard_sizes, out)
+        if rank == 0:
+            out["sharded"] = sharded
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline and args.air == "perm":
+            out["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    dist.close()
+    return 0
 
+
+def device_of(args, dist) -> int:
+    if args.device is not None:
+        return args.device
+    import ctypes
+    from linea_stark_prover_amd import _lib
+    n = ctypes.c_int()
+    _lib.check(_lib.lib().lsp_device_count(ctypes.byref(n)))
+    return dist.local_rank % max(n.value, 1)
+
+
+def main_leg(args, dist, ranks_seen):
     from linea_stark_prover_amd.air import permutation_air
     from linea_stark_prover_amd.prover import Context, StarkConfig, gen_permutation_trace, gen_wide_trace
+    from linea_stark_prover_amd.replicas import rank_seed, timed_steps
+    import numpy as np
 
+    world, rank = dist.world, dist.rank
     shard = args.shard
-    if shard:
-        from linea_stark_prover_amd import shard as S  # imports torch before the HIP library loads
     cfg = StarkConfig(seed=args.seed)
-    ctx = Context(cfg, device=local if args.device is None else args.device)
+    ctx = Context(cfg, device=device_of(args, dist))
     if shard:
+        from linea_stark_prover_amd import shard as S
         if args.comm == "rccl":
             S.attach_rccl(ctx)
         else:
@@ -100,50 +198,50 @@ def main():
     dtrace = ctx.dev_alloc(trace.nbytes)
     ctx.h2d(dtrace, trace)  # resident in HBM before the timed region
 
-    phases_acc = {}
+    phases_acc, step_s = {}, []
 
     def record():
         for name, ms in ctx.last_timings():
             phases_acc[name] = phases_acc.get(name, 0.0) + ms
 
     if shard:
+        from linea_stark_prover_amd import shard as S
         step = lambda: S.prove_sharded(ctx, dtrace, air, pub, h, w)  # noqa: E731
     else:
         step = lambda: ctx.prove(dtrace, air, pub, h, w)  # noqa: E731
-    elapsed, proof = timed_steps(step, args.steps, args.warmup, dist, sync=ctx.synchronize, on_step=record)
+    elapsed, proof = timed_steps(step, args.steps, args.warmup, dist, sync=ctx.synchronize, on_step=record,
+                                 step_times=step_s)
     phases = {k: v / max(args.steps, 1) for k, v in phases_acc.items()}
     verified = ctx.verify(proof, air, pub) if proof is not None else False
-
     if rank == 0 and args.dump_proof and proof is not None:
         with open(args.dump_proof, "wb") as f:
             f.write(proof)
+
+    out = None
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = (1 if shard else world) * h * args.steps / elapsed
         N = h << cfg.log_blowup
-        import ctypes
-        from linea_stark_prover_amd import _lib
-        desc = (ctypes.c_int32 * len(air.descriptor()))(*air.descriptor())
-        lq = ctypes.c_uint32()
-        _lib.check(_lib.lib().lsp_log_quotient_degree(desc, len(desc), cfg.public_degree, ctypes.byref(lq)))
-        q = 1 << lq.value
+        q = 1 << air_log_q(air, cfg)
         lde_ms = phases.get("coset_lde_batch", float("nan"))
         Nr = N // world if shard else N  # LDE rows (Merkle leaves) this rank computes
         lde_bytes = 32 * w * (h + Nr)
         achieved = lde_bytes / (lde_ms * 1e-3) / 1e9
         merkle_ms = phases.get("merkle tree", float("nan"))
         trace_perms = Nr * ((w + 1) // 2) + (Nr - 1)
-        calib = ctx.calibrate_poseidon2()
         valu_achieved = trace_perms / (merkle_ms * 1e-3) / 1e6
+        peak = valu_peak()
         out = {
             "metric": METRIC,
             "value": value,
             "unit": "trace-rows/s",
             "n_gpus": world,
+            "n_ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "prove_time_s": ms_per_step / 1e3,
+            "prove_time_median_s": statistics.median(step_s) if step_s else None,
             "higher_is_better": True,
             "scaling": "strong" if shard else "weak",
             "vs_baseline": value / PUBLISHED_ROWS_PER_S,
@@ -157,31 +255,149 @@ def main():
                                    f"{cfg.log_blowup}, {cfg.num_queries} queries, Poseidon2-w3 Merkle, FRI)",
                        "log_n": args.log_n, "width": w, "fri_queries": cfg.num_queries,
                        "parallelism": (f"sharded{world} ({args.comm})" if shard else
-                                       "replicas" if world > 1 else "single-gpu")},
+                                       f"replicas{world}" if world > 1 else "single-gpu")},
             "verified": bool(verified),
             "phases_ms": {k: round(v, 3) for k, v in phases.items()},
             "roofline": {"bound": "hbm", "kernel": "coset_lde_batch (trace, w x 2^log_n -> 8x)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": lde_traffic(args.log_n, w),
                          "valu_issue": valu_issue(["k_ntt_rm"]),
-                         "note": "VALU-bound: valu_issue = share of the chip's VALU issue slots the NTT passes "
+                         "note": "VALU-bound: valu_issue = share of the chip's VALU issue cycles the NTT passes "
                                  "use (PMC, profiles/*_valu_pmc.json); HBM frac is low by design",
                          "algorithmic_bytes": lde_bytes, "ms": lde_ms},
             "roofline_valu": {"bound": "valu", "kernel": "trace Merkle tree (Poseidon2 leaf hash + levels)",
                               "achieved": valu_achieved, "unit": "M perm/s",
-                              "peak": calib, "frac": valu_achieved / calib,
-                              "peak_source": "lsp_calibrate_poseidon2: register-resident chained permutations",
+                              "peak": peak["mperm_per_s"] if peak else None,
+                              "frac": valu_achieved / peak["mperm_per_s"] if peak else None,
+                              "frac_at_measured_clock": (valu_achieved / peak["mperm_per_s_at_measured_clock"]
+                                                         if peak else None),
+                              "peak_source": peak["source"] if peak else "profiles/r02_rates.json missing",
+                              "fr_mul_achieved_g_per_s": valu_achieved * FR_MUL_PER_PERM / 1e3,
+                              "fr_mul_peak_g_per_s": peak["gfrmul_per_s"] if peak else None,
+                              "calibrated_register_resident_mperm_per_s": ctx.calibrate_poseidon2(),
                               "valu_issue": valu_issue(["k_hash_rows1<11u, false>", "k_merkle_level<11u, false>"]),
-                              "perms": trace_perms, "fr_mul_per_perm": 230, "ms": merkle_ms},
+                              "perms": trace_perms, "fr_mul_per_perm": FR_MUL_PER_PERM, "ms": merkle_ms},
         }
         if world == 1 and not shard and args.inflight > 1:
             out["inflight"] = inflight(args, cfg, air, pub, trace, ctx, dtrace)
-        if world == 1 and not args.no_cpu_baseline and args.air == "perm":
-            out["cpu_baseline"] = cpu_baseline(args)
-        print(json.dumps(out), flush=True)
+        if world == 1 and not shard and not args.no_host_trace_leg:
+            out["prove_time_host_trace_s"] = host_trace_leg(args, ctx, trace, air, pub)
+            out["rows_per_s_host_trace"] = h / out["prove_time_host_trace_s"]["median"]
     ctx.dev_free(dtrace)
-    ctx.close()
-    dist.close()
+    return out, ctx
+
+
+def air_log_q(air, cfg) -> int:
+    import ctypes
+    from linea_stark_prover_amd import _lib
+    desc = (ctypes.c_int32 * len(air.descriptor()))(*air.descriptor())
+    lq = ctypes.c_uint32()
+    _lib.check(_lib.lib().lsp_log_quotient_degree(desc, len(desc), cfg.public_degree, ctypes.byref(lq)))
+    return lq.value
+
+
+def host_trace_leg(args, ctx, trace, air, pub):
+    """SURVEY 8(d) rows/s: wall time including the H2D of the trace (pageable
+    host array -> HBM inside lsp_prove), K steps after W warmups."""
+    for _ in range(max(args.warmup, 1)):
+        ctx.prove(trace, air, pub)
+    ts = []
+    for _ in range(max(args.steps, 1)):
+        t = time.perf_counter()
+        ctx.prove(trace, air, pub)
+        ts.append(time.perf_counter() - t)
+    return {"mean": sum(ts) / len(ts), "median": statistics.median(ts), "steps": len(ts),
+            "trace_bytes": int(trace.nbytes),
+            "note": "the trace starts in pageable host memory each step; value above starts with it in HBM"}
+
+
+def shard_leg_sizes(args, world):
+    if args.shard_leg == "none" or args.shard or args.air != "perm":
+        return []
+    if args.shard_leg == "auto":
+        return [24] + ([26] if world == 8 else [])
+    return [int(x) for x in args.shard_leg.split(",") if x]
+
+
+def guarded_shard_leg(args, dist, ctx, sizes, out):
+    """Run the C4 leg under a per-rank watchdog: if any collective hangs, rank
+    0 still prints the main line (with the failure noted) and every rank exits."""
+    done = threading.Event()
+
+    def watchdog():
+        if done.wait(args.shard_timeout):
+            return
+        if dist.rank == 0 and out is not None:
+            out["sharded"] = {"error": f"sharded leg exceeded {args.shard_timeout:.0f} s on rank 0; abandoned"}
+            print(json.dumps(out), flush=True)
+        os._exit(0 if dist.rank == 0 else 3)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+    try:
+        return shard_leg(args, dist, ctx, sizes)
+    except Exception as e:  # the main line is still reported
+        return {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        done.set()
+
+
+def shard_leg(args, dist, ctx, sizes):
+    """one proof per size sharded over every rank."""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.replicas import timed_steps
+    from linea_stark_prover_amd.prover import StarkConfig
+    import ctypes
+    import numpy as np
+    from linea_stark_prover_amd import _lib
+
+    world, rank = dist.world, dist.rank
+    cfg = StarkConfig(seed=args.seed)
+    a, d, _ = cfg.seeded()
+    pub = np.concatenate([a, d])
+    air = permutation_air(args.ncols)
+    w = 2 * args.ncols + 2
+    comm = "solo"
+    if world > 1:
+        from linea_stark_prover_amd import shard as S
+        ndev = ctypes.c_int()
+        _lib.check(_lib.lib().lsp_device_count(ctypes.byref(ndev)))
+        comm = args.shard_comm
+        if comm == "auto":
+            local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+            comm = "rccl" if ndev.value >= local_world and args.device is None else "gloo"
+        if comm == "rccl":
+            S.attach_rccl(ctx)
+        else:
+            S.GlooComm().attach(ctx)
+        seen = ctx.comm_info()[1]  # after the attach's allgather/bcast self-test
+    else:
+        seen = 1
+    res = {"comm": comm, "n_ranks_seen": seen, "scaling": "strong", "runs": []}
+    for log_n in sizes:
+        h = 1 << log_n
+        dtrace = ctx.gen_permutation_trace_device(log_n, args.ncols, a, d, seed=args.seed)
+        if world > 1:
+            from linea_stark_prover_amd import shard as S
+            step = lambda: S.prove_sharded(ctx, dtrace, air, pub, h, w)  # noqa: E731
+        else:
+            step = lambda: ctx.prove(dtrace, air, pub, h, w)  # noqa: E731
+        elapsed, proof = timed_steps(step, args.shard_leg_steps, args.shard_leg_warmup, dist,
+                                     sync=ctx.synchronize)
+        ctx.dev_free(dtrace)
+        run = {"log_n": log_n, "rows": h, "steps": args.shard_leg_steps, "warmup": args.shard_leg_warmup,
+               "prove_time_s": elapsed / args.shard_leg_steps,
+               "value": h * args.shard_leg_steps / elapsed, "unit": "trace-rows/s",
+               "workload": f"{args.ncols}x{args.ncols} permutation AIR, 2^{log_n} rows, one proof over {world} "
+                           f"rank(s)", "proof_bytes": len(proof) if proof else 0}
+        if rank == 0:
+            t = time.perf_counter()
+            run["verified"] = bool(ctx.verify(proof, air, pub))
+            run["verify_s"] = time.perf_counter() - t
+        res["runs"].append(run)
+    if world > 1:
+        from linea_stark_prover_amd import shard as S
+        S.detach(ctx)
+    return res
 
 
 def inflight(args, cfg, air, pub, trace, ctx, dtrace):
@@ -190,13 +406,12 @@ def inflight(args, cfg, air, pub, trace, ctx, dtrace):
     latency-bound phases (narrow Merkle levels, transcript, tree tops) overlap
     another's hashing.  Reported beside `value` (the sequential single-proof
     rate), never instead of it."""
-    import threading
     from linea_stark_prover_amd.prover import Context
     P, K = args.inflight, max(args.steps, 2)
     h, w = trace.shape[0], trace.shape[1]
     ctxs, ptrs = [ctx], [dtrace]
     for _ in range(P - 1):
-        c = Context(cfg, device=ctx_device(ctx, args))
+        c = Context(cfg, device=ctx.device)
         p = c.dev_alloc(trace.nbytes)
         c.h2d(p, trace)
         c.prove(p, air, pub, h, w)  # warm
@@ -224,14 +439,32 @@ def inflight(args, cfg, air, pub, trace, ctx, dtrace):
             "note": "independent proofs on P streams of one GPU; value above is one proof at a time"}
 
 
-def ctx_device(ctx, args):
-    return int(os.environ.get("LOCAL_RANK", "0")) if args.device is None else args.device
+def valu_peak():
+    """Chip peak for Poseidon2 hashing from the committed instruction-rate
+    probe: v_mad_u64_u32 at C cycles per wave64 per SIMD (profiles/
+    r02_rates.json) -> SIMDS * 64 / C MADs per cycle; one Fr product = 128 MADs
+    (8 x 32-bit limbs), one permutation = 230 products.  At the nominal 2.4 GHz
+    and at the clock the probe's MAD loop held."""
+    try:
+        r = json.load(open(RATES_FILE))
+    except (OSError, ValueError):
+        return None
+    cyc = r["peak_basis"]["v_mad_u64_u32_cycles"]
+    ghz_meas = r["peak_basis"]["measured_ghz"]
+    mads = SIMDS * 64 / cyc * NOMINAL_GHZ * 1e9
+    perm = mads / (MAD_PER_FR_MUL * FR_MUL_PER_PERM)
+    return {"mad_per_s": mads, "gfrmul_per_s": mads / MAD_PER_FR_MUL / 1e9, "mperm_per_s": perm / 1e6,
+            "mperm_per_s_at_measured_clock": perm / 1e6 * ghz_meas / NOMINAL_GHZ,
+            "source": f"profiles/r02_rates.json: v_mad_u64_u32 {cyc} cycles per wave64 per SIMD x {SIMDS} SIMDs "
+                      f"at {NOMINAL_GHZ} GHz; {MAD_PER_FR_MUL} MADs per Fr product, {FR_MUL_PER_PERM} products "
+                      f"per permutation (measured clock under MAD load {ghz_meas} GHz)"}
 
 
 def valu_issue(kernels):
-    """Calls-weighted VALU issue utilisation of the named kernels from the
-    committed PMC passes (tools/pmc_valu.sh -> profiles/*_valu_pmc.json, 2^19
-    prove): SQ_INSTS_VALU * 4 / (1024 SIMDs * cycles); None if absent."""
+    """Time-weighted VALU issue utilisation of the named kernels from the
+    committed PMC passes (tools/pmc_valu.sh -> profiles/*_valu_pmc.json):
+    issue cycles (each instruction class at its measured cost,
+    profiles/r02_rates.json) / (1024 SIMDs x kernel cycles); None if absent."""
     import glob
     d = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu_pmc.json"))):
@@ -262,22 +495,50 @@ def lde_traffic(log_n, w):
     return best
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_share() -> int:
+    """the host cores this process may use: the scheduler affinity, capped by the
+    pool's per-GPU share (OMP_NUM_THREADS / nproc on the GPU box)"""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(n, omp) if omp > 0 else n
+
+
 def cpu_baseline(args):
-    """The oracle's C restatement proving a bounded sample of the same workload
-    on the host (test infrastructure used only as the reported baseline)."""
+    """The oracle's C restatement proving the headline workload (2^cpu_log_n
+    rows) on the host (test infrastructure used only as the reported
+    baseline), one thread per core of this process's CPU share."""
     from oracle import cref
     cref.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = cpu_share()
     p = cref.setup(args.seed)
     tb, w = cref.gen_perm_trace(p, args.cpu_log_n, args.ncols, seed=args.seed)
     t = time.perf_counter()
     cref.prove(p, tb, 1 << args.cpu_log_n, w, cref.perm_air(args.ncols), nthreads=threads)
     dt = time.perf_counter() - t
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
+    except (OSError, ValueError):
+        nproc = None
     return {"value": (1 << args.cpu_log_n) / dt, "unit": "trace-rows/s", "cores": threads, "kind": "port",
-            "seconds": dt,
+            "seconds": dt, "nproc": nproc, "machine_cpus": os.cpu_count(), "cpu_model": cpu_model(),
             "sample": f"oracle/lsp_oracle.c full prove, {args.ncols}x{args.ncols} permutation AIR at "
-                      f"2^{args.cpu_log_n} rows (same conventions/seed), {threads} threads"}
+                      f"2^{args.cpu_log_n} rows (the headline workload, same conventions/seed), {threads} threads "
+                      f"= this process's CPU share (affinity / OMP_NUM_THREADS)"}
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

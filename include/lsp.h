@@ -243,6 +243,8 @@ int lsp_ctx_detach_comm(lsp_ctx *ctx);
 /* collective check of the attached communicator: an allgather and a
  * broadcast of known patterns (LSP_E_STATE on wrong data) */
 int lsp_comm_selftest(lsp_ctx *ctx);
+/* rank and size of the attached communicator (LSP_E_STATE if none) */
+int lsp_comm_info(lsp_ctx *ctx, int *rank, int *size);
 int lsp_prove_sharded(lsp_ctx *ctx, const lsp_fr *trace, size_t h, size_t w, const int32_t *air, size_t air_len,
                       const lsp_fr *public_values, size_t npub, int mem, lsp_proof **out);
 /* serialized proof (format in DESIGN.md); buf == NULL -> *len = required size */
@@ -310,6 +312,16 @@ int lsp_calibrate_poseidon2(lsp_ctx *ctx, double *mperm_per_s);
  * row-major h x (2*ncols + 2), h = 2^log_n. */
 int lsp_gen_permutation_trace(uint64_t seed, uint32_t log_n, uint32_t ncols, const lsp_fr *alpha,
                               const lsp_fr *delta, int small_values, lsp_fr *rows_out);
+
+/* The same workload shape generated on the device, for sizes where a host
+ * trace would hold tens of GiB per rank (bench.py's sharded 2^24-2^26 leg):
+ * raw columns a = seeded hash values < 2^252, b = a with rows shuffled by a
+ * seeded bijection i -> (mul i + add) mod 2^log_n, then the permutation
+ * witness (lsp_witness_permutation) into the row-major device trace of
+ * 2^log_n x (2 ncols + 2) elements.  Not the host generator's values (that
+ * one uses Fisher-Yates); deterministic in the seed, identical on every rank. */
+int lsp_gen_permutation_trace_device(lsp_ctx *ctx, uint64_t seed, uint32_t log_n, uint32_t ncols,
+                                     const lsp_fr *alpha, const lsp_fr *delta, lsp_fr *trace_dev);
 
 /* Synthetic wide trace (stand-in for the missing zkevm.bin):
  * nlookup LogUp lookups (RawLookupTrace::get_trace, trace/src/lookup.rs:46-176;

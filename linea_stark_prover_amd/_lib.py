@@ -102,6 +102,7 @@ _SIGS = {
     "lsp_ctx_attach_rccl": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "lsp_ctx_detach_comm": (ctypes.c_int, [ctypes.c_void_p]),
     "lsp_comm_selftest": (ctypes.c_int, [ctypes.c_void_p]),
+    "lsp_comm_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "lsp_prove_sharded": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
                                          ctypes.c_size_t, c_fr_p, ctypes.c_size_t, ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_void_p)]),
@@ -140,6 +141,8 @@ _SIGS = {
     "lsp_calibrate_poseidon2": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "lsp_gen_permutation_trace": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, c_fr_p, c_fr_p,
                                                  ctypes.c_int, c_fr_p]),
+    "lsp_gen_permutation_trace_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                                        ctypes.c_uint32, c_fr_p, c_fr_p, c_fr_p]),
 }
 
 EXPORTED = sorted(_SIGS)

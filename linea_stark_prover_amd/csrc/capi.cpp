@@ -778,6 +778,16 @@ int lsp_comm_selftest(lsp_ctx* ctx) {
     });
 }
 
+int lsp_comm_info(lsp_ctx* ctx, int* rank, int* size) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && rank && size, LSP_E_ARG, "null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        LSP_REQUIRE(ctx->comm, LSP_E_STATE, "no communicator attached");
+        *rank = ctx->comm->rank;
+        *size = ctx->comm->size;
+    });
+}
+
 int lsp_ctx_detach_comm(lsp_ctx* ctx) {
     return guarded(ctx, [&] {
         LSP_REQUIRE(ctx, LSP_E_ARG, "null ctx");
@@ -905,6 +915,27 @@ int lsp_witness_permutation(lsp_ctx* ctx, const lsp_fr* a, uint32_t na, const ls
         witness_block(ctx, trace, n, trace_w, col0, (size_t)na + nb + 2, mem, [&](Fr* out, size_t stride) {
             witness_permutation_device(ctx, da, na, db, nb, n, al, de, out, stride);
         });
+    });
+}
+
+int lsp_gen_permutation_trace_device(lsp_ctx* ctx, uint64_t seed, uint32_t log_n, uint32_t ncols,
+                                     const lsp_fr* alpha, const lsp_fr* delta, lsp_fr* trace) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && alpha && delta && trace && ncols >= 1 && log_n >= 1 && log_n <= 30, LSP_E_ARG,
+                    "bad device trace-generator arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        const size_t n = (size_t)1 << log_n;
+        Fr* a = ctx->fbuf("gen_a", (size_t)ncols * n);
+        Fr* b = ctx->fbuf("gen_b", (size_t)ncols * n);
+        // the row bijection i -> (mul i + add) mod n: mul odd, both from the seed
+        const uint64_t mul = ((seed * 0xD1B54A32D192ED03ull) ^ 0x5851F42D4C957F2Dull) | 1u;
+        const uint64_t add = seed * 0xA24BAED4963EE407ull + 0x9FB21C651E98DF25ull;
+        LSP_HIP(launch_gen_raw_perm(seed, n, ncols, mul, add, a, b, ctx->stream));
+        witness_permutation_device(ctx, a, ncols, b, ncols, n, to_fr(*alpha), to_fr(*delta), (Fr*)trace,
+                                   2 * (size_t)ncols + 2);
+        ctx->release("gen_");
+        ctx->release("wit_");
     });
 }
 

@@ -320,6 +320,18 @@ void* lsp_ctx::buf(const std::string& name, size_t bytes) {
     return b.p;
 }
 
+void lsp_ctx::release(const std::string& prefix) {
+    LSP_HIP(hipStreamSynchronize(stream));
+    for (auto it = pool.begin(); it != pool.end();) {
+        if (it->first.compare(0, prefix.size(), prefix) == 0) {
+            if (it->second.p) LSP_HIP(hipFree(it->second.p));
+            it = pool.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+
 void* lsp_ctx::hbuf(const std::string& name, size_t bytes) {
     Buf& b = hpool[name];
     if (b.cap < bytes) {

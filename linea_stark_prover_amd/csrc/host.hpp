@@ -287,6 +287,8 @@ struct lsp_ctx {
 
     void* buf(const std::string& name, size_t bytes);
     lsp::Fr* fbuf(const std::string& name, size_t n) { return (lsp::Fr*)buf(name, n * sizeof(lsp::Fr)); }
+    // drain the stream and free every pooled buffer whose name starts with `prefix`
+    void release(const std::string& prefix);
     // scratch of a hierarchical batch inverse of n elements (launch_batch_inverse)
     lsp::Fr* bi_scratch(size_t n) { return fbuf("bi_scratch", lsp::batch_inverse_scratch(n) + 1); }
     // pinned host memory; growing it first drains the stream (a copy may still read it)

@@ -191,12 +191,53 @@ hipError_t with_temp(Scratch s, F&& f) {
     if (need > s.cap) return hipErrorInvalidValue;
     return f(s.p, need);
 }
+
+// Synthetic raw permutation columns generated on the device (bench inputs at
+// sizes where a host generator would hold tens of GiB per rank): a[c][i] is a
+// counter-based hash of (seed, c, i) masked to 252 bits (< r), in Montgomery
+// form; b[c][i] = a[c][pi(i)] with the row bijection pi(i) = (mul i + add)
+// mod n (mul odd), the same for every column -- B is a row shuffle of A, as
+// the permutation argument requires.  Deterministic in the seed, so every
+// rank of a sharded proof builds the same trace without moving it.
+__device__ __forceinline__ uint64_t smix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ Fr gen_value(uint64_t seed, uint32_t c, size_t i) {
+    Fr x;
+    const uint64_t base = seed * 0x9E3779B97F4A7C15ull + ((uint64_t)c << 40) + ((uint64_t)i << 2);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t v = smix(base + (uint64_t)k + 0x632BE59BD9B4E019ull);
+        x.v[2 * k] = (uint32_t)v;
+        x.v[2 * k + 1] = (uint32_t)(v >> 32);
+    }
+    x.v[7] &= (1u << 28) - 1;  // < 2^252 < r
+    return fr_mul(x, fr_r2());
+}
+__global__ __launch_bounds__(256) void k_gen_raw_perm(uint64_t seed, size_t n, uint32_t ncols, uint64_t mul,
+                                                      uint64_t add, Fr* __restrict__ a, Fr* __restrict__ b) {
+    const size_t i = gtid();
+    if (i >= n) return;
+    const size_t j = (size_t)((mul * (uint64_t)i + add) & (uint64_t)(n - 1));
+    for (uint32_t c = 0; c < ncols; ++c) {
+        a[c * n + i] = gen_value(seed, c, i);
+        b[c * n + i] = gen_value(seed, c, j);
+    }
+}
 }  // namespace
 
 size_t witness_scratch_bytes(size_t n, uint32_t nt) {
     // sort keys/perms (double buffered) + run starts + hipCUB temp (generous bound)
     const size_t m = n * (1 + (size_t)nt);
     return m * (2 * sizeof(uint64_t) + 2 * sizeof(uint32_t) + 2 * sizeof(uint64_t)) + 6 * 256 + (64u << 20) + m * 64;
+}
+
+hipError_t launch_gen_raw_perm(uint64_t seed, size_t n, uint32_t ncols, uint64_t mul, uint64_t add, Fr* a, Fr* b,
+                               hipStream_t st) {
+    hipLaunchKernelGGL(k_gen_raw_perm, dim3(nblocks(n, 256)), dim3(256), 0, st, seed, n, ncols, mul, add, a, b);
+    return hipGetLastError();
 }
 
 hipError_t launch_perm_rows(const Fr* a, uint32_t na, const Fr* b, uint32_t nb, size_t n, Fr alpha, Fr delta,

@@ -91,6 +91,10 @@ hipError_t launch_assemble_chunks(const Fr* stage, uint32_t logGq, size_t cpr, s
 // ----------------------------------------------------- k_witness.hip
 // (trace crate semantics; see k_witness.hip)
 size_t witness_scratch_bytes(size_t n, uint32_t ntables);
+// synthetic raw permutation columns (ncols x n each, column-major): a = seeded
+// hash values, b[c][i] = a[c][(mul i + add) mod n]; n a power of two, mul odd
+hipError_t launch_gen_raw_perm(uint64_t seed, size_t n, uint32_t ncols, uint64_t mul, uint64_t add, Fr* a, Fr* b,
+                               hipStream_t st);
 // trace row i (stride ostride): a cols, b cols; al/bl = row combination + delta
 hipError_t launch_perm_rows(const Fr* a, uint32_t na, const Fr* b, uint32_t nb, size_t n, Fr alpha, Fr delta,
                             Fr* out, size_t ostride, Fr* al, Fr* bl, hipStream_t st);

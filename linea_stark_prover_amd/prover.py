@@ -79,6 +79,7 @@ class Context:
     def __init__(self, config: StarkConfig = StarkConfig(), device: int = 0,
                  round_constants: Optional[np.ndarray] = None):
         self.config = config
+        self.device = device
         if round_constants is None:
             _, _, round_constants = config.seeded()
         self._rc = _fr_arr(round_constants)
@@ -241,6 +242,27 @@ class Context:
         v = ctypes.c_double()
         self._chk(L.lib().lsp_calibrate_fr_mul(self.h, ctypes.byref(v)))
         return v.value
+
+    def gen_permutation_trace_device(self, log_n: int, ncols: int, alpha: np.ndarray, delta: np.ndarray,
+                                     seed: int = DEFAULT_SEED) -> int:
+        """The C1 workload shape generated on the device (lsp_gen_permutation_trace_device):
+        returns a device pointer to the (2^log_n, 2*ncols+2) row-major trace; free it with
+        dev_free.  Values differ from gen_permutation_trace's (see include/lsp.h)."""
+        w = 2 * ncols + 2
+        p = self.dev_alloc((1 << log_n) * w * 32)
+        try:
+            self._chk(L.lib().lsp_gen_permutation_trace_device(self.h, seed, log_n, ncols, _ptr(_fr_arr(alpha)),
+                                                               _ptr(_fr_arr(delta)), p))
+        except BaseException:
+            self.dev_free(p)
+            raise
+        return p
+
+    def comm_info(self) -> Tuple[int, int]:
+        """(rank, size) of the attached communicator"""
+        r, n = ctypes.c_int(), ctypes.c_int()
+        self._chk(L.lib().lsp_comm_info(self.h, ctypes.byref(r), ctypes.byref(n)))
+        return r.value, n.value
 
     def calibrate_poseidon2(self) -> float:
         """M Poseidon2 permutations/s (register-resident chained states)."""

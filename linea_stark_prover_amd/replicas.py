@@ -35,6 +35,14 @@ class Dist:
         self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
         return float(t.item())
 
+    def sum(self, x: float) -> float:
+        if self.pg is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
+        return float(t.item())
+
     def close(self):
         if self.pg is not None:
             self.pg.destroy_process_group()
@@ -55,9 +63,12 @@ def init_from_env() -> Dist:
 
 
 def timed_steps(step: Callable[[], object], steps: int, warmup: int, d: Dist,
-                sync: Callable[[], None] = lambda: None, on_step: Callable[[], None] = lambda: None):
+                sync: Callable[[], None] = lambda: None, on_step: Callable[[], None] = lambda: None,
+                step_times: Optional[list] = None):
     """W untimed steps, barrier + sync, K timed steps, sync + barrier; returns
-    (max-over-ranks elapsed seconds, last step result)."""
+    (max-over-ranks elapsed seconds, last step result).  `step_times` (if given)
+    receives this rank's wall time of every timed step (the step itself
+    returns with its result on the host)."""
     out = None
     for _ in range(warmup):
         out = step()
@@ -65,7 +76,10 @@ def timed_steps(step: Callable[[], object], steps: int, warmup: int, d: Dist,
     sync()
     t0 = time.perf_counter()
     for _ in range(steps):
+        ts = time.perf_counter()
         out = step()
+        if step_times is not None:
+            step_times.append(time.perf_counter() - ts)
         on_step()
     sync()
     d.barrier()

@@ -20,8 +20,8 @@ def _run(tmp_path, nproc, comm, port, log_n=10):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", LSP_FRI_SHARD_MIN="16")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--shard", "--comm", comm, "--device", "0", "--log-n", str(log_n), "--steps", "1", "--warmup", "0",
-           "--no-cpu-baseline", "--dump-proof", str(out)]
+           "--gpus", str(nproc), "--shard", "--comm", comm, "--device", "0", "--log-n", str(log_n), "--steps", "1",
+           "--warmup", "0", "--no-cpu-baseline", "--dump-proof", str(out)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     return out.read_bytes()
@@ -47,3 +47,48 @@ def test_rccl_transport_single_rank(gpu_ctx, tmp_path):
     """RCCL loads (dlopen), initialises and carries the sharded prove's
     collectives; one rank because RCCL needs a GPU per rank"""
     assert _run(tmp_path, 1, "rccl", 29613) == _single(gpu_ctx)
+
+
+def _bench_json(args, timeout=420):
+    import json
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                       text=True, timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    return lines[0]
+
+
+def test_bench_gpus2_shard_spawns_ranks():
+    """bench.py --gpus 2 started without a launcher runs two
+    ranks (here both on the box's one GPU over gloo) and reports n_gpus 2"""
+    o = _bench_json(["--gpus", "2", "--shard", "--comm", "gloo", "--log-n", "12", "--steps", "1", "--warmup", "1",
+                     "--no-cpu-baseline", "--shard-leg", "none"])
+    assert o["n_gpus"] == 2 and o["n_ranks_seen"] == 2 and o["verified"] is True
+    assert o["scaling"] == "strong"
+
+
+def test_bench_sharded_leg_two_ranks():
+    """the C4 'sharded' field: one device-generated trace proved by two ranks
+    (gloo, sharing one GPU) verifies; the replicas value beside it is weak scaling"""
+    o = _bench_json(["--gpus", "2", "--log-n", "10", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
+                     "--shard-leg", "12,13", "--shard-leg-steps", "1", "--shard-leg-warmup", "0"])
+    assert o["n_gpus"] == 2 and o["scaling"] == "weak" and o["verified"] is True
+    sh = o["sharded"]
+    assert sh["comm"] == "gloo" and sh["n_ranks_seen"] == 2, sh
+    assert [r["log_n"] for r in sh["runs"]] == [12, 13]
+    assert all(r["verified"] for r in sh["runs"])
+
+
+def test_bench_sharded_leg_single_gpu_equals_prove():
+    """N = 1: the sharded field is lsp_prove itself (prove_shard over SoloComm),
+    and the device-generated trace proves and verifies"""
+    o = _bench_json(["--log-n", "10", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--inflight", "0",
+                     "--shard-leg", "14", "--shard-leg-steps", "2"])
+    sh = o["sharded"]
+    assert sh["comm"] == "solo" and sh["n_ranks_seen"] == 1
+    assert sh["runs"][0]["verified"] is True
+    assert o["prove_time_host_trace_s"]["median"] > 0

@@ -66,3 +66,31 @@ def test_single_process_default(product_lib):
     from linea_stark_prover_amd.replicas import Dist, timed_steps
     el, out = timed_steps(lambda: 7, 2, 1, Dist())
     assert out == 7 and el >= 0
+
+
+def _bench(args, env_extra=None, timeout=240):
+    env = dict(os.environ, **(env_extra or {}))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        if not env_extra or k not in env_extra:
+            env.pop(k, None)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout, cwd=ROOT)
+
+
+def test_gpus_2_without_launcher_spawns_two_ranks():
+    """bench.py --gpus 2 started bare runs torch.distributed.run with two ranks
+    (never one rank reported as two GPUs); --dry-run stops before any GPU work"""
+    import json
+    r = _bench(["--gpus", "2", "--dry-run"])
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["n_ranks_seen"] == 2
+    assert lines[0]["launcher"] == "torch.distributed.run"
+
+
+def test_world_size_mismatch_is_an_error():
+    import json
+    r = _bench(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2
+    assert "refusing" in json.loads(r.stdout.strip().splitlines()[-1])["error"]

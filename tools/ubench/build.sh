@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build the microbenchmarks from source (binaries are git-ignored; they travel
+# to the GPU box with the gpurun snapshot).  Usage: tools/ubench/build.sh [name...]
+set -e
+cd "$(dirname "$0")"
+HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
+names=${*:-"rates p2bench mulbench"}
+for n in $names; do
+    case $n in
+        host_perm) g++ -O3 -march=native -std=c++17 -o host_perm_bin host_perm.cpp ;;
+        *) $HIPCC --offload-arch=gfx950 -O3 -std=c++17 -o "$n" "$n.hip" ;;
+    esac
+done

@@ -52,15 +52,36 @@ __device__ __forceinline__ constexpr uint32_t p29(int i) {
 #define LSP_F29_USE_ASM 1
 #endif
 
+// C = (2^261 - 1) mod r in 29-bit limbs: the constant the folded quotient
+// digits below add to every product (tools/gen_fr29mul.py C29)
+__device__ __forceinline__ constexpr uint32_t c29(int i) {
+    return i == 0 ? 0x1ffffe49u
+         : i == 1 ? 0x1077ffffu
+         : i == 2 ? 0x1fff8e31u
+         : i == 3 ? 0x10d0103fu
+         : i == 4 ? 0xddb0965u
+         : i == 5 ? 0x7071c5cu
+         : i == 6 ? 0x18da2e10u
+         : i == 7 ? 0x486f3a3u
+         : i == 8 ? 0xec090u
+                  : 0u;
+}
+
 // Montgomery product a * b * 2^-261 mod r.  FIPS, one 64-bit accumulator.
-// r = 1 mod 2^29, so the quotient digit can be m_k = -t mod 2^32 (a full
-// word: no mask) and m_k * r[0] = m_k clears the low 29 bits of the column.
-// Column sums stay < 2^63.2 (tools/gen_fr29mul.py --bound); the quotient
-// M = sum m_k 2^(29k) < 2^264, so the output is < a b / 2^261 + 8 r.
+// r = 1 mod 2^29, so the quotient digit of column k can be any m'_k with
+// acc + m'_k = -1 mod 2^29.  We take m'_k = ~acc mod 2^32 (a full word: no
+// mask, and m'_k * r[0] = m'_k is never multiplied): acc + m'_k =
+// (acc_hi + 1) 2^32 - 1, whose floor by 2^29 -- the carry -- is acc_hi * 8 + 7
+// (one MAD of the high word, which also adds the next column's constant).
+// Every low column of T = a b + C + M' r then ends in 29 one-bits, so the upper
+// columns yield Q = (T + 1) / 2^261 - 1, and with C = (2^261 - 1) mod r (added
+// limb by limb through the carries) Q == a b 2^-261 (mod r).
+// Column sums stay < 2^63.2 (tools/gen_fr29mul.py --bound); M' < 2^264, so the
+// output is < a b / 2^261 + 8 r + 1.
 __device__ __forceinline__ F29 f29_mul_c(const F29& a, const F29& b) {
     uint32_t m[9];
     F29 o;
-    uint64_t acc = 0;
+    uint64_t acc = c29(0);
 #pragma unroll
     for (int k = 0; k < 9; ++k) {
 #pragma unroll
@@ -69,8 +90,8 @@ __device__ __forceinline__ F29 f29_mul_c(const F29& a, const F29& b) {
             acc += (uint64_t)m[j] * p29(k - j);
         }
         acc += (uint64_t)a.l[k] * b.l[0];
-        m[k] = 0u - (uint32_t)acc;
-        acc = (acc + m[k]) >> 29;
+        m[k] = ~(uint32_t)acc;
+        acc = (acc >> 32) * 8 + 7 + c29(k + 1);
     }
 #pragma unroll
     for (int k = 9; k < 17; ++k) {
@@ -94,7 +115,7 @@ __device__ __forceinline__ F29 f29_sqr_c(const F29& a) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) d[i] = a.l[i] << 1;
     F29 o;
-    uint64_t acc = 0;
+    uint64_t acc = c29(0);
 #pragma unroll
     for (int k = 0; k < 17; ++k) {
 #pragma unroll
@@ -103,8 +124,8 @@ __device__ __forceinline__ F29 f29_sqr_c(const F29& a) {
 #pragma unroll
         for (int j = (k > 8 ? k - 8 : 0); j < (k < 9 ? k : 9); ++j) acc += (uint64_t)m[j] * p29(k - j);
         if (k < 9) {
-            m[k] = 0u - (uint32_t)acc;
-            acc = (acc + m[k]) >> 29;
+            m[k] = ~(uint32_t)acc;
+            acc = (acc >> 32) * 8 + 7 + c29(k + 1);
         } else {
             o.l[k - 9] = (uint32_t)acc & F29_MASK;
             acc >>= 29;

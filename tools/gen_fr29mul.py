@@ -100,19 +100,36 @@ def gen(kind, chains):
 
 ACC = "v[2:3]"   # block mode: the accumulator lives in a fixed, clobbered VGPR pair
 ACC_LO = "v2"
+ACC_HI = "v3"
+R_MOD = sum(p << (29 * i) for i, p in enumerate(P29))
+# the folded-digit form (--block): C = (2^261 - 1) mod r, added into the
+# columns as constants (fr29.hpp, f29_mul_c)
+C_OFF = ((1 << 261) - 1) % R_MOD
+C29 = [(C_OFF >> (29 * i)) & ((1 << 29) - 1) for i in range(8)] + [C_OFF >> 232]
 
 
 def gen_block(kind):
     """the whole product as ONE asm statement: the compiler inserts its
     conservative hazard s_nop after every asm statement whose result the next
-    instruction reads; inside one statement there are none"""
+    instruction reads; inside one statement there are none.
+
+    Folded quotient digits (no MAD by r[0] = 1, no 64-bit shift): in a low
+    column the digit is m'_k = ~acc mod 2^32, so acc + m'_k = (acc_hi + 1) 2^32
+    - 1 and its floor by 2^29 is acc_hi * 8 + 7: one v_mad_u64_u32 of the high
+    word by 8 that also adds the next column's constant c_(k+1) + 7.  Each low
+    column of T = a b + C + M' r then ends in 29 one-bits, so the upper columns
+    give Q = (T + 1) / 2^261 - 1 == a b 2^-261 (mod r) for C = (2^261 - 1) mod r
+    (fr29.hpp f29_mul_c states the same in C)."""
     sq = kind == "sqr"
     name = "f29_sqr_asm" if sq else "f29_mul_asm"
     sig = "(const F29& a)" if sq else "(const F29& a, const F29& b)"
     out = [f"__device__ __forceinline__ F29 {name}{sig} {{"]
     out.append("    uint32_t m0, m1, m2, m3, m4, m5, m6, m7, m8;")
     if sq:
-        out.append("    const uint32_t " + ", ".join(f"d{i} = a.l[{i}] << 1" for i in range(9)) + ";")
+        # 2 a_i as v_add_u32 (2-cycle issue; the compiler's x << 1 is a 4-cycle v_lshlrev_b32)
+        out.append("    uint32_t " + ", ".join(f"d{i}" for i in range(9)) + ";")
+        for i in range(9):
+            out.append(f'    asm("v_add_u32 %0, %1, %1" : "=v"(d{i}) : "v"(a.l[{i}]));')
     out.append("    F29 o;")
     out.append("    uint64_t c;")
     lines, ins = [], {}
@@ -134,16 +151,15 @@ def gen_block(kind):
             if 1 <= k - j <= 8:
                 terms.append((f"m{j}", f"p{k - j}"))
         for x, y in terms:
-            src2 = "0" if first else ACC
+            src2 = "%[k0]" if first else ACC
             first = False
             lines.append(f"v_mad_u64_u32 {ACC}, %[c], %[{x}], %[{y}], {src2}")
             for o in (x, y):
                 if not o.startswith("m"):
                     ins[o] = True
         if k < 9:
-            lines.append(f"v_sub_u32 %[m{k}], 0, {ACC_LO}")
-            lines.append(f"v_mad_u64_u32 {ACC}, %[c], %[m{k}], 1, {ACC}")
-            lines.append(f"v_lshrrev_b64 {ACC}, 29, {ACC}")
+            lines.append(f"v_not_b32 %[m{k}], {ACC_LO}")
+            lines.append(f"v_mad_u64_u32 {ACC}, %[c], {ACC_HI}, 8, %[k{k + 1}]")
         else:
             lines.append(f"v_and_b32 %[o{k - 9}], %[mask], {ACC_LO}")
             lines.append(f"v_lshrrev_b64 {ACC}, 29, {ACC}")
@@ -152,8 +168,10 @@ def gen_block(kind):
     for l in lines:
         out.append(f'        "{l}\\n\\t"')
     outs = [f'[m{k}] "=&v"(m{k})' for k in range(9)] + [f'[o{k}] "=&v"(o.l[{k}])' for k in range(9)] + ['[c] "=&s"(c)']
+    consts = [f'[k0] "s"({hex(C29[0])}ull)'] + \
+             [f'[k{k}] "s"({hex((C29[k] if k < 9 else 0) + 7)}ull)' for k in range(1, 10)]
     out.append("        : " + ", ".join(outs))
-    out.append("        : " + ", ".join([operand(o) for o in ins] + ['[mask] "s"(0x1fffffffu)']))
+    out.append("        : " + ", ".join([operand(o) for o in ins] + ['[mask] "s"(0x1fffffffu)'] + consts))
     out.append('        : "v2", "v3");')
     out.append("    (void)c;")
     out.append("    (void)m0; (void)m1; (void)m2; (void)m3; (void)m4; (void)m5; (void)m6; (void)m7; (void)m8;")

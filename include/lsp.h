@@ -249,13 +249,71 @@ int lsp_prove_sharded(lsp_ctx *ctx, const lsp_fr *trace, size_t h, size_t w, con
                       const lsp_fr *public_values, size_t npub, int mem, lsp_proof **out);
 /* serialized proof (format in DESIGN.md); buf == NULL -> *len = required size */
 int lsp_proof_serialize(const lsp_proof *proof, uint8_t *buf, size_t cap, size_t *len);
+/* the inverse (untrusted bytes: LSP_E_ARG on anything malformed) */
+int lsp_proof_deserialize(const uint8_t *buf, size_t len, lsp_proof **out);
 int lsp_proof_free(lsp_proof *proof);
+
+/* ------------------------------------------------------------- Proof<SC> */
+/* Field-by-field view of a proof, one field per field of
+ * p3_uni_stark::Proof<SC> ([EXT p3-uni-stark proof.rs]; built at
+ * bin/src/main.rs:80-86, read by p3_uni_stark::verify at bin/src/main.rs:88-96)
+ * for the reference's Config (bin/src/config.rs:19-25: Val = Challenge = Fr,
+ * MerkleTreeMmcs<Val,Val,Hash,Compress,1>, TwoAdicFriPcs):
+ *   degree_bits                         <- degree_bits
+ *   commitments.trace                   <- Hash::from([*trace_commit])
+ *   commitments.quotient_chunks         <- Hash::from([*quotient_commit])
+ *   opened_values.trace_local / _next   <- trace_local[width] / trace_next[width]
+ *   opened_values.quotient_chunks[j]    <- vec![quotient_chunks[j]]   (j < 2^log_quotient_chunks)
+ *   opening_proof: FriProof {
+ *     commit_phase_commits[r]           <- Hash::from([fri_commits[r]])
+ *     final_poly                        <- final_poly[final_poly_len]
+ *     pow_witness                       <- *pow_witness
+ *     query_proofs[i]: QueryProof {
+ *       input_proof: vec![               (one BatchOpening per committed round)
+ *         BatchOpening { opened_values: vec![trace_rows[i]],
+ *                        opening_proof: trace_paths[i] as Vec<[Fr; 1]> },
+ *         BatchOpening { opened_values: (0..q).map(|j| vec![quotient_rows[i][j]]),
+ *                        opening_proof: quotient_paths[i] as Vec<[Fr; 1]> } ],
+ *       commit_phase_openings[r]: CommitPhaseProofStep {
+ *         sibling_value: fri_siblings[i][r],
+ *         opening_proof: fri_paths[i][r] (fri_path_lens[r] digests) } } }
+ * Arrays are query-major (query i's trace row at trace_rows + i*width, its
+ * round-r FRI path after the paths of rounds < r); paths list siblings leaf
+ * to root.  Elements are lsp_fr (Montgomery, canonical).  The pointers stay
+ * valid until lsp_proof_free.  rust/p3-hip/src/proof.rs builds Proof<SC>
+ * from this view and back. */
+typedef struct {
+    uint32_t degree_bits;          /* log2 of the trace height */
+    uint32_t log_quotient_chunks;  /* q = 2^log_quotient_chunks */
+    uint32_t width;                /* trace width w */
+    uint32_t num_queries;
+    uint32_t num_fri_rounds;
+    uint32_t final_poly_len;
+    uint32_t input_path_len;       /* Merkle path length of the trace and quotient openings */
+    const uint32_t *fri_path_lens; /* [num_fri_rounds] */
+    const lsp_fr *trace_commit, *quotient_commit, *pow_witness;
+    const lsp_fr *trace_local, *trace_next, *quotient_chunks;
+    const lsp_fr *fri_commits, *final_poly;
+    const lsp_fr *trace_rows, *trace_paths;        /* num_queries x width, num_queries x input_path_len */
+    const lsp_fr *quotient_rows, *quotient_paths;  /* num_queries x q, num_queries x input_path_len */
+    const lsp_fr *fri_siblings, *fri_paths;        /* num_queries x rounds, num_queries x sum(fri_path_lens) */
+} lsp_proof_view;
+int lsp_proof_get_view(const lsp_proof *proof, lsp_proof_view *view);
+/* a proof handle from a view (copies; e.g. a Proof<SC> made elsewhere, for
+ * lsp_proof_serialize / lsp_verify); LSP_E_ARG on null or non-canonical data */
+int lsp_proof_from_view(const lsp_proof_view *view, lsp_proof **out);
 /* p3_uni_stark::verify (bin/src/main.rs:88-96) on the host CPU */
 int lsp_verify(const lsp_ctx *ctx, const int32_t *air, size_t air_len, const lsp_fr *public_values, size_t npub,
                const uint8_t *proof, size_t len);
 /* per-phase device times of the last lsp_prove (ms), span names as in the
  * reference's bench.log */
 int lsp_last_timings(const lsp_ctx *ctx, double *ms, const char **names, size_t cap, size_t *n);
+/* the last lsp_prove's data-shaped operations in order, worded as the
+ * reference's tracing spans with dims (bench.log:19-64), e.g.
+ * "coset_lde_batch dims: 14x524288 | added_bits: 3",
+ * "reduce matrix quotient dims: 1x4194304", "divide_by_height dims: 1x8";
+ * strings live until the next prove on ctx */
+int lsp_last_spans(const lsp_ctx *ctx, const char **lines, size_t cap, size_t *n);
 
 /* Witness generation on the device: the trace crate's
  * RawPermutationTrace::get_trace (trace/src/permutation.rs:24-93) and

@@ -97,6 +97,9 @@ _SIGS = {
     "lsp_proof_serialize": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                            ctypes.POINTER(ctypes.c_size_t)]),
     "lsp_proof_free": (ctypes.c_int, [ctypes.c_void_p]),
+    "lsp_proof_deserialize": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    "lsp_proof_get_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),  # lsp_proof_view* (proof.py)
+    "lsp_proof_from_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "lsp_ctx_attach_comm_ops": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(LspCommOps)]),
     "lsp_comm_rccl_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "lsp_ctx_attach_rccl": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
@@ -117,6 +120,8 @@ _SIGS = {
     "lsp_last_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t,
                                         ctypes.POINTER(ctypes.c_size_t)]),
+    "lsp_last_spans": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t,
+                                      ctypes.POINTER(ctypes.c_size_t)]),
     "lsp_gen_wide_trace": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, c_fr_p, c_fr_p, c_fr_p,
                                           ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,

@@ -25,7 +25,7 @@ ARCH = os.environ.get("LSP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["k_ntt.hip", "k_hash.hip", "k_field.hip", "k_quotient.hip", "k_open.hip", "k_witness.hip",
-           "host.cpp", "host_ifma.cpp", "prove.cpp", "verify.cpp", "witness.cpp", "cbor.cpp", "comm_ext.cpp", "capi.cpp"]
+           "host.cpp", "host_ifma.cpp", "prove.cpp", "verify.cpp", "proof.cpp", "witness.cpp", "cbor.cpp", "comm_ext.cpp", "capi.cpp"]
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
           # host code: mulx/adcx/adox for the 4 x 64-bit host multiplier (x86-64 with BMI2 + ADX:
           # the build container and the MI355X hosts)

@@ -825,6 +825,29 @@ int lsp_proof_serialize(const lsp_proof* p, uint8_t* buf, size_t cap, size_t* le
     });
 }
 
+int lsp_proof_deserialize(const uint8_t* buf, size_t len, lsp_proof** out) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(buf && out, LSP_E_ARG, "null");
+        *out = nullptr;
+        *out = deserialize(buf, len);
+    });
+}
+
+int lsp_proof_get_view(const lsp_proof* p, lsp_proof_view* view) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(p && view, LSP_E_ARG, "null");
+        proof_view(*p, view);
+    });
+}
+
+int lsp_proof_from_view(const lsp_proof_view* view, lsp_proof** out) {
+    return guarded(nullptr, [&] {
+        LSP_REQUIRE(view && out, LSP_E_ARG, "null");
+        *out = nullptr;
+        *out = proof_from_view(*view);
+    });
+}
+
 int lsp_proof_free(lsp_proof* p) {
     delete p;
     return LSP_OK;
@@ -854,6 +877,14 @@ int lsp_last_timings(const lsp_ctx* ctx, double* ms, const char** names, size_t 
         if (ms) ms[i] = ctx->timings[i].second;
         if (names) names[i] = ctx->timings[i].first.c_str();
     }
+    return LSP_OK;
+}
+
+int lsp_last_spans(const lsp_ctx* ctx, const char** lines, size_t cap, size_t* n) {
+    if (!ctx || !n) return LSP_E_ARG;
+    *n = ctx->spans.size();
+    for (size_t i = 0; i < ctx->spans.size() && i < cap; ++i)
+        if (lines) lines[i] = ctx->spans[i].c_str();
     return LSP_OK;
 }
 

@@ -191,6 +191,7 @@ struct lsp_proof {
     std::vector<lsp::Fr> tl, tn, qc, roots, final_poly;
     std::vector<lsp::lsp_query> queries;
     mutable std::vector<uint8_t> wire;  // serialize() result, cached by lsp_proof_serialize
+    mutable std::shared_ptr<void> view_cache;  // flat arrays behind lsp_proof_view (proof.cpp)
 };
 
 // a parsed CBOR RawPermutationTrace / RawLookupTrace (cbor.cpp)
@@ -284,6 +285,9 @@ struct lsp_ctx {
     std::map<uint32_t, std::vector<lsp::Fr>> fold_tw;  // host FRI fold factors g^-bitrev(i) per log2 length (prove.cpp)
     size_t fri_host_tail = 2048;  // FRI rounds of at most this many leaves run wholly on the host (prove.cpp)
     std::vector<std::pair<std::string, double>> timings;
+    // the last proof's data-shaped spans in the reference's bench.log wording
+    // (prove.cpp; lsp_last_spans)
+    std::vector<std::string> spans;
 
     void* buf(const std::string& name, size_t bytes);
     lsp::Fr* fbuf(const std::string& name, size_t n) { return (lsp::Fr*)buf(name, n * sizeof(lsp::Fr)); }

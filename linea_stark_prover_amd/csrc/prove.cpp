@@ -438,6 +438,18 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
     const Fr one = fr_one();
     PhaseTimer T(ctx);
     auto* proof = new lsp_proof();
+    // the logical operations of p3_uni_stark::prove with their dims, worded as
+    // the reference's tracing spans (bench.log:19-64); batched launches below
+    // are logged per reference call (one quotient chunk, one opened matrix)
+    ctx->spans.clear();
+    auto span = [&](const char* name, size_t rows_w, size_t height, int added_bits) {
+        char s[160];
+        if (added_bits >= 0)
+            std::snprintf(s, sizeof s, "%s dims: %zux%zu | added_bits: %d", name, rows_w, height, added_bits);
+        else
+            std::snprintf(s, sizeof s, "%s dims: %zux%zu", name, rows_w, height);
+        ctx->spans.emplace_back(s);
+    };
     proof->log_h = log_h;
     proof->log_q = log_q;
     proof->w = (uint32_t)w;
@@ -448,6 +460,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         Fr* lde = ctx->fbuf("t_lde", S * w);
         std::vector<Fr> shifts(std::max(w, q), GEN);
         T.begin("coset_lde_batch");
+        span("coset_lde_batch", w, h, (int)lb);
         lde_device(ctx, d_trace, h, w, lb, shifts.data(), lde, k0, nk);
         T.end("coset_lde_batch");
         Fr* tlay = ctx->fbuf("t_tree", 2 * S - 1);
@@ -550,6 +563,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         }
         Fr* qlde = ctx->fbuf("q_lde", S * q);
         T.begin("coset_lde_batch (quotient)");
+        for (size_t j = 0; j < q; ++j) span("coset_lde_batch", 1, h, (int)lb);  // one launch, q independent columns
         lde_device(ctx, qv, h, q, lb, shifts.data(), qlde, k0, nk);
         T.end("coset_lde_batch (quotient)");
         Fr* qlay = ctx->fbuf("q_tree", 2 * S - 1);
@@ -605,6 +619,12 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         T.end("compute opened values with Lagrange interpolation");
 
         T.begin("reduce rows");
+        // the (matrix, point) order of TwoAdicFriPcs::open that the reduction
+        // below folds in (k_reduce_rows): trace at zeta, trace at zeta*w_h,
+        // then quotient chunk j at zeta
+        span("reduce matrix quotient", w, N, -1);
+        span("reduce matrix quotient", w, N, -1);
+        for (size_t j = 0; j < q; ++j) span("reduce matrix quotient", 1, N, -1);
         std::vector<Fr> apw(2 * w + q);
         apw[0] = one;
         for (size_t k = 1; k < apw.size(); ++k) apw[k] = fr_mul(apw[k - 1], alpha_fri);
@@ -796,6 +816,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         T.end("commit phase");
         {
             // final poly: bit-reverse, IDFT (naive, len <= 2^lb small), truncate
+            span("divide_by_height", 1, len, -1);
             const uint32_t lgl = log2_exact(len);
             std::vector<Fr> br(len);
             for (size_t i = 0; i < len; ++i) br[i] = fin[host_bitrev(i, lgl)];
@@ -924,68 +945,6 @@ lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, con
                         size_t npub) {
     SoloComm solo;
     return prove_shard(ctx, solo, d_trace, h, w, air, pub, npub);
-}
-
-// --------------------------------------------------------- serialization
-// little-endian words and canonical field elements, written in one pass into a
-// buffer sized up front
-namespace {
-struct Writer {
-    uint8_t* p;
-    void u32(uint32_t x) {
-        for (int i = 0; i < 4; ++i) *p++ = (uint8_t)(x >> (8 * i));
-    }
-    void fr(const Fr& x) {
-        // Montgomery form -> integer: a product by 1 on the 4 x 64-bit host multiplier
-        const hp64::F one{{1, 0, 0, 0}};
-        const Fr c = hp64::to_canonical(hp64::mul(hp64::from(x), one));
-        std::memcpy(p, c.v, 32);  // 32-bit words little-endian (x86-64 host)
-        p += 32;
-    }
-    void frs(const std::vector<Fr>& v) {
-        for (auto& x : v) fr(x);
-    }
-};
-}  // namespace
-
-std::vector<uint8_t> serialize(const lsp_proof& p) {
-    size_t nfr = 3 + p.tl.size() + p.tn.size() + p.qc.size() + p.roots.size() + p.final_poly.size(), nu32 = 5;
-    for (auto& q : p.queries) {
-        nfr += q.trow.size() + q.tpath.size() + q.qrow.size() + q.qpath.size() + q.sib.size();
-        for (auto& f : q.fpath) nfr += f.size();
-        nu32 += 2 + q.sib.size();
-    }
-    std::vector<uint8_t> b(8 + 4 * nu32 + 32 * nfr);
-    std::memcpy(b.data(), "LSPPRF01", 8);
-    Writer w{b.data() + 8};
-    w.u32(p.log_h);
-    w.u32(p.log_q);
-    w.u32(p.w);
-    w.u32((uint32_t)p.queries.size());
-    w.u32((uint32_t)p.roots.size());
-    w.fr(p.troot);
-    w.fr(p.qroot);
-    w.frs(p.tl);
-    w.frs(p.tn);
-    w.frs(p.qc);
-    w.frs(p.roots);
-    w.frs(p.final_poly);
-    w.fr(p.pow_w);
-    for (auto& q : p.queries) {
-        w.frs(q.trow);
-        w.u32((uint32_t)q.tpath.size());
-        w.frs(q.tpath);
-        w.frs(q.qrow);
-        w.u32((uint32_t)q.qpath.size());
-        w.frs(q.qpath);
-        for (size_t r = 0; r < q.sib.size(); ++r) {
-            w.fr(q.sib[r]);
-            w.u32((uint32_t)q.fpath[r].size());
-            w.frs(q.fpath[r]);
-        }
-    }
-    if (w.p != b.data() + b.size()) throw LspError(LSP_E_STATE, "proof serialization size mismatch");
-    return b;
 }
 
 }  // namespace lsp

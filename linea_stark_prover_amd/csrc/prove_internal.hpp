@@ -19,7 +19,11 @@ struct Comm;
 // every rank returns the same proof
 lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, size_t w, const Air& air,
                        const Fr* pub, size_t npub);
+// proof wire format and field view (proof.cpp)
 std::vector<uint8_t> serialize(const lsp_proof& p);
+lsp_proof* deserialize(const uint8_t* buf, size_t len);
+void proof_view(const lsp_proof& p, lsp_proof_view* v);
+lsp_proof* proof_from_view(const lsp_proof_view& v);
 // communicators of a process-per-GPU sharded prove (comm_ext.cpp)
 Comm* make_callback_comm(const lsp_comm_ops& ops);
 void rccl_unique_id(uint8_t out[128]);

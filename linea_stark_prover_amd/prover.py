@@ -278,6 +278,14 @@ class Context:
         L.lib().lsp_last_timings(self.h, ms, names, n.value, ctypes.byref(n))
         return [(names[i].decode(), ms[i]) for i in range(n.value)]
 
+    def last_spans(self) -> List[str]:
+        """the last proof's operations with dims, in the reference's bench.log wording"""
+        n = ctypes.c_size_t()
+        self._chk(L.lib().lsp_last_spans(self.h, None, 0, ctypes.byref(n)))
+        lines = (ctypes.c_char_p * n.value)()
+        self._chk(L.lib().lsp_last_spans(self.h, lines, n.value, ctypes.byref(n)))
+        return [lines[i].decode() for i in range(n.value)]
+
 
 class Radix2DitParallel:
     """TwoAdicSubgroupDft (bin/src/config.rs:22) on the GPU; returns the

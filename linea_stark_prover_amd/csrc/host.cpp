@@ -398,8 +398,9 @@ const uint4* lsp_ctx::twiddle29(uint32_t logH, bool inverse) {
     Fr* pw = fbuf("tw_pow_tmp", half);
     LSP_HIP(launch_powers(tab, L1, half, pw, stream));
     uint4* out = nullptr;
-    LSP_HIP(hipMalloc(&out, half * 3 * sizeof(uint4)));
-    LSP_HIP(launch_to_f29limbs(pw, out, half, stream));
+    const size_t n = logH ? (size_t(1) << logH) - 1 : 1;
+    LSP_HIP(hipMalloc(&out, n * 3 * sizeof(uint4)));
+    LSP_HIP(launch_stage_twiddles(pw, logH, out, stream));
     LSP_HIP(hipStreamSynchronize(stream));
     twiddles[key] = out;
     return out;

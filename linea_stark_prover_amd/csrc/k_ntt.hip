@@ -24,6 +24,9 @@
 // normalised and < 8.3 r (sums reduced to < 2r, products < 8.06 r); a - b is
 // formed carry-free as a + 16r - b (f29_sub16).  Between passes the arrays hold
 // ark words reduced to < 2r; only the last forward pass writes canonical words.
+#include <algorithm>
+#include <cstdlib>
+
 #include "fr29.hpp"
 #include "k_common.hpp"
 #include "kernels.hpp"
@@ -31,18 +34,22 @@
 namespace lsp {
 
 namespace {
-enum PassMode : int { PASS_INPLACE = 0, PASS_INV_FIRST = 1, PASS_FWD_FIRST = 2 };
+// PASS_INV_FWD: the inverse transform's last pass fused with the forward's first (k_ntt_rm)
+enum PassMode : int { PASS_INPLACE = 0, PASS_INV_FIRST = 1, PASS_INV_FWD = 2 };
 
 struct NttPass {
-    const Fr* src;      // PASS_INV_FIRST: caller rows; PASS_FWD_FIRST: X (coefficients)
+    const Fr* src;      // PASS_INV_FIRST: caller rows; PASS_INV_FWD: X after the earlier inverse passes (or caller rows)
     Fr* dst;            // the arrays being transformed (h rows each, batch of `narr` arrays, row-major w)
-    const uint4* tw;    // w_H^x (or inverse), x < H/2: 29-bit limbs, 3 x uint4 per element
-    const Fr* twist;    // PASS_FWD_FIRST: two-level tables per (coset[, column])
+    const uint4* tw;    // stage-major twiddles (launch_stage_twiddles), 29-bit limbs, 3 x uint4 per element
+    const uint4* tw_inv;  // PASS_INV_FWD: the inverse transform's twiddles
+    uint32_t inv_gather;  // PASS_INV_FWD: the inverse has only this pass (src = caller rows, gathered bit-reversed)
+    const Fr* twist;    // PASS_INV_FWD: two-level tables per (coset[, column])
     uint32_t L1, L2;    // twist table split
     uint32_t twist_per_col;  // 1: table index k*w + c, 0: table index k
     uint32_t logH, s0, k, logL, logG, w;
     uint32_t nchunk;    // column chunks of 2^LOGCW per row
     uint32_t canon;     // 1: write canonical words (the transform's last pass)
+    uint32_t xcd;       // 1: workgroup ids map to tiles XCD-aware (see k_ntt_rm)
     uint64_t narr;      // arrays (cosets) in dst
 };
 
@@ -69,25 +76,226 @@ __device__ __forceinline__ Fr f29_store(const F29& v, bool canon) {
     return canon ? fr_reduce_once(o) : o;
 }
 
+// carry propagation only (no modular reduction): limbs < 2^32 - 2^3 in,
+// limbs 0..7 < 2^29 out, same integer
+__device__ __forceinline__ F29 f29_norm(const F29& a) {
+    F29 o;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t s = a.l[i] + c;
+        o.l[i] = s & F29_MASK;
+        c = s >> 29;
+    }
+    o.l[8] = a.l[8] + c;
+    return o;
+}
+
+// a + 32 r - b limb-wise (as f29_sub16): b normalised with value < 32 r;
+// limbs < 1.5 2^30, a valid product operand up to ~60 r
+// (tools/gen_fr29mul.py --bound checks the column sums)
+__device__ __forceinline__ F29 f29_sub32(const F29& a, const F29& b) {
+    constexpr uint32_t L[9] = {0x20000020u, 0x317fffffu, 0x2000084fu, 0x3dbfb3ffu, 0x2002b353u,
+                               0x31e5c37au, 0x2b305a25u, 0x3a68b294u, 0x2556caau};
+    F29 o;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o.l[i] = a.l[i] + L[i] - b.l[i];
+    return o;
+}
+
+// The tile in LDS as three planes (limbs 0-3, limbs 4-7, limb 8), so an
+// element is one ds_read_b128 + ds_read_b128 + ds_read_b32 at any index
+// (a 36-byte array element is only 4-byte aligned: 5 narrow reads)
+struct TileLds {
+    uint4* a;
+    uint4* b;
+    uint32_t* c;
+    __device__ __forceinline__ F29 get(uint32_t e) const {
+        const uint4 x = a[e], y = b[e];
+        F29 o;
+        o.l[0] = x.x; o.l[1] = x.y; o.l[2] = x.z; o.l[3] = x.w;
+        o.l[4] = y.x; o.l[5] = y.y; o.l[6] = y.z; o.l[7] = y.w;
+        o.l[8] = c[e];
+        return o;
+    }
+    __device__ __forceinline__ void put(uint32_t e, const F29& v) const {
+        a[e] = make_uint4(v.l[0], v.l[1], v.l[2], v.l[3]);
+        b[e] = make_uint4(v.l[4], v.l[5], v.l[6], v.l[7]);
+        c[e] = v.l[8];
+    }
+};
+
+// Two radix-2 stages in registers (radix-4 groups): per group 4 elements are
+// read from and written to the LDS once instead of twice, one barrier per two
+// stages, 3 twiddles per 4 butterflies, and the sums between the two stages
+// only carry-normalised.  Invariant between groups: normalised and < 8.3 r.
+//
+// DIF stages s (distance D) and s + 1 (D/2) on v0..v3 = positions t0, t0 + D/2,
+// t0 + D, t0 + 3D/2: wA = w(s, t0), wA2 = w(s, t0 + D/2), wB = w(s + 1, t0)
+// (= w(s + 1, t0 + D)); trivB: stage s + 1 is the transform's last (w = 1).
+__device__ __forceinline__ void dif4(F29& v0, F29& v1, F29& v2, F29& v3, const F29& wA, const F29& wA2,
+                                     const F29& wB, bool trivB) {
+    const F29 u0 = f29_norm(f29_lazy2(v0, v2));       // < 16.6 r
+    const F29 u2 = f29_mul(f29_sub16(v0, v2), wA);    // < 8.06 r
+    const F29 u1 = f29_norm(f29_lazy2(v1, v3));
+    const F29 u3 = f29_mul(f29_sub16(v1, v3), wA2);
+    v0 = f29_reduce(f29_lazy2(u0, u1));               // < 2 r
+    v2 = f29_reduce(f29_lazy2(u2, u3));
+    if (trivB) {
+        v1 = f29_reduce(f29_sub32(u0, u1));
+        v3 = f29_reduce(f29_sub16(u2, u3));
+    } else {
+        v1 = f29_mul(f29_sub32(u0, u1), wB);          // < 48.6 r in -> < 8.11 r
+        v3 = f29_mul(f29_sub16(u2, u3), wB);
+    }
+}
+
+// DIT stages s (distance d) and s + 1 (2d) on v0..v3 = positions t0, t0 + d,
+// t0 + 2d, t0 + 3d: wA = w(s, t0) (= w(s, t0 + 2d)), wB = w(s + 1, t0),
+// wB2 = w(s + 1, t0 + d); trivA: stage s is the transform's first (w = 1).
+__device__ __forceinline__ void dit4(F29& v0, F29& v1, F29& v2, F29& v3, const F29& wA, const F29& wB,
+                                     const F29& wB2, bool trivA) {
+    const F29 p1 = trivA ? v1 : f29_mul(v1, wA);      // < 8.3 r
+    const F29 p3 = trivA ? v3 : f29_mul(v3, wA);
+    const F29 u0 = f29_lazy2(v0, p1);                 // limbs < 2^30, < 16.6 r
+    const F29 u1 = f29_sub16(v0, p1);                 // limbs < 1.5 2^30, < 24.6 r
+    const F29 u2 = f29_lazy2(v2, p3);
+    const F29 u3 = f29_sub16(v2, p3);
+    const F29 q2 = f29_mul(u2, wB);                   // < 8.07 r
+    const F29 q3 = f29_mul(u3, wB2);
+    v0 = f29_reduce(f29_lazy2(u0, q2));               // < 2 r
+    v2 = f29_reduce(f29_sub16(u0, q2));
+    v1 = f29_reduce(f29_lazy2(u1, q3));
+    v3 = f29_reduce(f29_sub16(u1, q3));
+}
+
 // One tile: 2^k positions x 2^logG groups x 2^LOGCW columns (power-of-two
 // chunk, so every index below is shifts and masks; rows are 32-bit within
-// an array, H <= 2^31).  The first forward pass (PASS_FWD_FIRST) runs one
-// workgroup per tile of the coefficients for ALL cosets: the tile is read
-// from X once into registers (<= 4 elements per thread) and twisted, transformed
-// and stored once per coset, so X is not re-read for every coset.
+// an array, H <= 2^31).  The first forward pass runs one workgroup per tile of
+// the coefficients for ALL cosets: the tile is kept in registers (<= 4
+// elements per thread) and twisted, transformed and stored once per coset, so
+// the coefficients are not re-read for every coset.  That pass is fused with
+// the inverse transform's last pass, which covers the same rows (stride
+// 2^(logH - k)): the coefficients never go to HBM.
 constexpr uint32_t NTT_THREADS = 256;
-constexpr uint32_t NTT_MAX_EL = 1024;  // 2^k x G x CW <= 2^7 x 8
+constexpr uint32_t NTT_MAX_EL = 1024;  // 2^k x G x CW
+
+template <int LOGCW>
+struct TileGeom {
+    uint32_t k, logG, logL, gid0;
+    __device__ __forceinline__ uint32_t row_of(uint32_t t, uint32_t g) const {
+        const uint32_t gid = gid0 + g;
+        return ((gid >> logL) << (logL + k)) + (t << logL) + (gid & ((1u << logL) - 1));
+    }
+    // element e of a thread-strided loop -> (position, group, column)
+    __device__ __forceinline__ void split(uint32_t e, uint32_t& t, uint32_t& g, uint32_t& c) const {
+        c = e & ((1u << LOGCW) - 1);
+        const uint32_t tg = e >> LOGCW;
+        if (logL < logG) {  // rows of adjacent positions are adjacent: position fastest
+            t = tg & ((1u << k) - 1);
+            g = tg >> k;
+        } else {
+            t = tg >> logG;
+            g = tg & ((1u << logG) - 1);
+        }
+    }
+    __device__ __forceinline__ uint32_t idx(uint32_t t, uint32_t g, uint32_t c) const {
+        return (((t << logG) + g) << LOGCW) + c;
+    }
+};
+
+// stages s0 .. s0 + k - 1 of the tile in LDS: radix-4 groups of two stages,
+// then a radix-2 stage if k is odd; ends with a barrier
+template <bool DIF, int LOGCW>
+__device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOGCW>& gm, const uint4* __restrict__ tw,
+                                            uint32_t s0, uint32_t logH, uint32_t n_el) {
+    constexpr uint32_t CW = 1u << LOGCW;
+    const uint32_t k = gm.k, G = 1u << gm.logG;
+    const uint32_t cshift = gm.logG + LOGCW;  // element index = (t << cshift) + (g << LOGCW) + c
+    const uint64_t H = 1ull << logH;
+    auto tw_at = [&](uint32_t row, uint32_t s) -> F29 {
+        // stage s uses the powers of w_(2^m), m = logH - s (DIF) or s + 1 (DIT):
+        // DIF w^((row mod H/2^(s+1)) 2^s), DIT w^((row mod 2^s) 2^(logH-1-s)); the
+        // table is stage-major (entry 2^(m-1) - 1 + i = w_(2^m)^i), so
+        // consecutive rows read consecutive slots
+        const uint32_t half = DIF ? (uint32_t)(H >> (s + 1)) : (1u << s);
+        return f29_load48(tw + 3 * (size_t)(half - 1 + (row & (half - 1))));
+    };
+    uint32_t j = 0;
+    for (; j + 1 < k; j += 2) {
+        const uint32_t s = s0 + j;
+        // the quad's members are t0 + m 2^b: DIF distances 2^(b+1), 2^b; DIT 2^b, 2^(b+1)
+        const uint32_t b = DIF ? (k - 2 - j) : j;
+        const uint32_t bmask = (1u << b) - 1;
+        const bool triv = DIF ? (s + 1 == logH - 1) : (s == 0);
+        for (uint32_t qd = threadIdx.x; qd < (n_el >> 2); qd += NTT_THREADS) {
+            const uint32_t c = qd & (CW - 1);
+            const uint32_t pg = qd >> LOGCW;
+            const uint32_t g = pg & (G - 1), pp = pg >> gm.logG;
+            const uint32_t t0 = ((pp & ~bmask) << 2) | (pp & bmask);
+            const uint32_t e0 = (t0 << cshift) + (g << LOGCW) + c, de = (1u << b) << cshift;
+            F29 v0 = T.get(e0), v1 = T.get(e0 + de), v2 = T.get(e0 + 2 * de), v3 = T.get(e0 + 3 * de);
+            const uint32_t r0 = gm.row_of(t0, g), dr = (1u << b) << gm.logL;
+            if (DIF)
+                dif4(v0, v1, v2, v3, tw_at(r0, s), tw_at(r0 + dr, s), triv ? v0 : tw_at(r0, s + 1), triv);
+            else
+                dit4(v0, v1, v2, v3, triv ? v0 : tw_at(r0, s), tw_at(r0, s + 1), tw_at(r0 + dr, s + 1), triv);
+            T.put(e0, v0);
+            T.put(e0 + de, v1);
+            T.put(e0 + 2 * de, v2);
+            T.put(e0 + 3 * de, v3);
+        }
+        __syncthreads();
+    }
+    if (j < k) {  // the last stage alone (odd k)
+        const uint32_t s = s0 + j;
+        const uint32_t logd = DIF ? 0u : j;
+        const bool trivial = DIF ? (s == logH - 1) : (s == 0);
+        const uint32_t dmask = (1u << logd) - 1;
+        for (uint32_t bf = threadIdx.x; bf < (n_el >> 1); bf += NTT_THREADS) {
+            const uint32_t c = bf & (CW - 1);
+            const uint32_t pg = bf >> LOGCW;
+            const uint32_t g = pg & (G - 1), pp = pg >> gm.logG;
+            const uint32_t t0 = ((pp >> logd) << (logd + 1)) | (pp & dmask);
+            const uint32_t a0 = (t0 << cshift) + (g << LOGCW) + c, a1 = a0 + ((1u << logd) << cshift);
+            const F29 a = T.get(a0), b = T.get(a1);
+            if (trivial) {
+                T.put(a0, f29_reduce(f29_lazy2(a, b)));
+                T.put(a1, f29_reduce(f29_sub16(a, b)));
+                continue;
+            }
+            const F29 wv = tw_at(gm.row_of(t0, g), s);
+            if (DIF) {
+                T.put(a0, f29_reduce(f29_lazy2(a, b)));
+                T.put(a1, f29_mul(f29_sub16(a, b), wv));
+            } else {
+                const F29 bw = f29_mul(b, wv);
+                T.put(a0, f29_reduce(f29_lazy2(a, bw)));
+                T.put(a1, f29_reduce(f29_sub16(a, bw)));
+            }
+        }
+        __syncthreads();
+    }
+}
 
 template <bool DIF, int MODE, int LOGCW>
 __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
-    extern __shared__ F29 lds[];
+    extern __shared__ uint4 lds_raw[];
     constexpr uint32_t CW = 1u << LOGCW;
-    constexpr bool FWD_FIRST = MODE == PASS_FWD_FIRST;
-    const uint32_t K = 1u << p.k, logG = p.logG, G = 1u << logG;
-    const uint32_t logL = p.logL, Lmask = (1u << logL) - 1, rowshift = logL + p.k;
+    constexpr bool FWD_FIRST = MODE == PASS_INV_FWD;
+    const uint32_t K = 1u << p.k, logG = p.logG;
     const uint64_t H = 1ull << p.logH;
     const uint32_t tiles_per_arr = (uint32_t)(H >> (p.k + logG)) * p.nchunk;
-    const uint32_t wg = blockIdx.x;
+    // Workgroups are dispatched round-robin over the 8 XCDs (each with its own
+    // L2).  With narrow column chunks a row's 256 bytes are read by nchunk
+    // workgroups: give all chunks of one tile to one XCD, back to back, so the
+    // row's lines are fetched from HBM once and served from that XCD's L2.
+    uint32_t wg = blockIdx.x;
+    if (p.xcd) {
+        const uint32_t x = wg & 7, i = wg >> 3;
+        const uint32_t tl = i / p.nchunk;
+        wg = ((tl << 3) + x) * p.nchunk + (i - tl * p.nchunk);
+    }
     const uint32_t arr0 = FWD_FIRST ? 0u : wg / tiles_per_arr;
     const uint32_t arr_end = FWD_FIRST ? (uint32_t)p.narr : arr0 + 1;
     const uint32_t rem = wg - arr0 * tiles_per_arr;
@@ -95,130 +303,87 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
     const uint32_t c0 = (rem - tile * p.nchunk) << LOGCW;
     const uint32_t cw = min(CW, p.w - c0);
     const uint32_t n_el = (K << logG) << LOGCW;
-    const bool t_minor = logL < logG;
-    const uint32_t gid0 = tile << logG;
-    auto row_of = [&](uint32_t t, uint32_t g) {
-        const uint32_t gid = gid0 + g;
-        return ((gid >> logL) << rowshift) + (t << logL) + (gid & Lmask);
-    };
-    auto split = [&](uint32_t e, uint32_t& t, uint32_t& g, uint32_t& c) {
-        c = e & (CW - 1);
-        const uint32_t tg = e >> LOGCW;
-        if (t_minor) {
-            t = tg & (K - 1);
-            g = tg >> p.k;
-        } else {
-            t = tg >> logG;
-            g = tg & (G - 1);
-        }
-    };
-    // ---- first forward pass: this thread's coefficients of the tile, read once
+    const TileGeom<LOGCW> gm{p.k, logG, p.logL, tile << logG};
+    const TileLds T{lds_raw, lds_raw + n_el, reinterpret_cast<uint32_t*>(lds_raw + 2 * n_el)};
     constexpr uint32_t NREG = FWD_FIRST ? NTT_MAX_EL / NTT_THREADS : 1;
     F29 xr[NREG];
     if (FWD_FIRST) {
+        // ---- the inverse transform's last stages over these rows (logH - k ..
+        // logH - 1; from the caller's rows, gathered bit-reversed, when the
+        // inverse has only this pass), then the coefficients (x h) stay in registers
+        for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
+            uint32_t t, g, c;
+            gm.split(e, t, g, c);
+            if (c >= cw) continue;
+            const uint32_t row = gm.row_of(t, g);
+            const uint32_t srow = p.inv_gather ? brev_bits(row, p.logH) : row;
+            T.put(gm.idx(t, g, c), f29_repack_in(p.src[(size_t)srow * p.w + c0 + c]));
+        }
+        __syncthreads();
+        tile_stages<false, LOGCW>(T, gm, p.tw_inv, p.logH - p.k, p.logH, n_el);
 #pragma unroll
         for (uint32_t j = 0; j < NREG; ++j) {
             const uint32_t e = threadIdx.x + j * NTT_THREADS;
             uint32_t t, g, c;
-            split(e, t, g, c);
-            if (e < n_el && c < cw) xr[j] = f29_repack_in(p.src[(size_t)row_of(t, g) * p.w + c0 + c]);
+            gm.split(e, t, g, c);
+            if (e < n_el && c < cw) xr[j] = T.get(gm.idx(t, g, c));  // normalised, < 8.3 r
         }
     }
-    F29* fac = lds + n_el;  // K * G extra entries (launcher sizes the LDS for it)
+    F29* fac = reinterpret_cast<F29*>(T.c + n_el);  // K * G extra entries (launcher sizes the LDS for it)
     const bool row_twist = FWD_FIRST && !p.twist_per_col;
     for (uint32_t arr = arr0; arr < arr_end; ++arr) {
         Fr* base = p.dst + (size_t)arr * H * p.w;
-        if (FWD_FIRST && arr > arr0) __syncthreads();  // the previous coset's stores have read the LDS
+        if (FWD_FIRST) __syncthreads();  // the previous reads of the tile are done
         // ---- twist factors s^row / h (29-bit form), once per row when every column shares the shift
         if (row_twist) {
             const Fr* tab = p.twist + (size_t)arr * ((1ull << p.L1) + (1ull << p.L2));
             for (uint32_t rg = threadIdx.x; rg < (K << logG); rg += NTT_THREADS) {
-                uint32_t t, g;
-                if (t_minor) {
-                    t = rg & (K - 1);
-                    g = rg >> p.k;
-                } else {
-                    t = rg >> logG;
-                    g = rg & (G - 1);
-                }
-                fac[(t << logG) + g] = pow2l29(tab, p.L1, row_of(t, g));
+                uint32_t t, g, c;
+                gm.split(rg << LOGCW, t, g, c);
+                fac[(t << logG) + g] = pow2l29(tab, p.L1, gm.row_of(t, g));
             }
             __syncthreads();
         }
-        // ---- load (optionally gathering / twisting)
+        // ---- load (twisting the registers, or from the array)
         if (FWD_FIRST) {
 #pragma unroll
             for (uint32_t j = 0; j < NREG; ++j) {
                 const uint32_t e = threadIdx.x + j * NTT_THREADS;
                 uint32_t t, g, c;
-                split(e, t, g, c);
+                gm.split(e, t, g, c);
                 if (e >= n_el || c >= cw) continue;
                 F29 f;
                 if (row_twist) {
                     f = fac[(t << logG) + g];
                 } else {
                     const Fr* tab = p.twist + ((size_t)arr * p.w + c0 + c) * ((1ull << p.L1) + (1ull << p.L2));
-                    f = pow2l29(tab, p.L1, row_of(t, g));
+                    f = pow2l29(tab, p.L1, gm.row_of(t, g));
                 }
-                lds[(((t << logG) + g) << LOGCW) + c] = f29_mul(xr[j], f);  // < 8.3 r
+                T.put(gm.idx(t, g, c), f29_mul(xr[j], f));  // < 8.3 r
             }
         } else {
             for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
                 uint32_t t, g, c;
-                split(e, t, g, c);
+                gm.split(e, t, g, c);
                 if (c >= cw) continue;
-                const uint32_t row = row_of(t, g);
+                const uint32_t row = gm.row_of(t, g);
                 F29 v;
                 if (MODE == PASS_INV_FIRST)
                     v = f29_repack_in(p.src[(size_t)brev_bits(row, p.logH) * p.w + c0 + c]);
                 else
                     v = f29_repack_in(base[(size_t)row * p.w + c0 + c]);
-                lds[(((t << logG) + g) << LOGCW) + c] = v;
+                T.put(gm.idx(t, g, c), v);
             }
         }
         __syncthreads();
-        // ---- k radix-2 stages
-        const uint32_t nbf = n_el >> 1;
-        for (uint32_t j = 0; j < p.k; ++j) {
-            const uint32_t s = p.s0 + j;
-            const uint32_t logd = DIF ? (p.k - 1 - j) : j;
-            const bool trivial = DIF ? (s == p.logH - 1) : (s == 0);
-            const uint32_t dmask = (1u << logd) - 1;
-            // twiddle index of butterfly row i0: DIF (i0 mod H/2^(s+1)) << s, DIT (i0 mod 2^s) << (logH-1-s)
-            const uint32_t tmask = DIF ? (uint32_t)((H >> (s + 1)) - 1) : ((1u << s) - 1);
-            const uint32_t tshift = DIF ? s : (p.logH - 1 - s);
-            for (uint32_t bf = threadIdx.x; bf < nbf; bf += NTT_THREADS) {
-                const uint32_t c = bf & (CW - 1);
-                const uint32_t pg = bf >> LOGCW;
-                const uint32_t g = pg & (G - 1), pp = pg >> logG;
-                const uint32_t t0 = ((pp >> logd) << (logd + 1)) | (pp & dmask);
-                const uint32_t t1 = t0 + (1u << logd);
-                const uint32_t a0 = (((t0 << logG) + g) << LOGCW) + c, a1 = (((t1 << logG) + g) << LOGCW) + c;
-                const F29 a = lds[a0], b = lds[a1];
-                if (trivial) {
-                    lds[a0] = f29_reduce(f29_lazy2(a, b));
-                    lds[a1] = f29_reduce(f29_sub16(a, b));
-                    continue;
-                }
-                const F29 wv = f29_load48(p.tw + 3 * (size_t)((row_of(t0, g) & tmask) << tshift));
-                if (DIF) {
-                    lds[a0] = f29_reduce(f29_lazy2(a, b));
-                    lds[a1] = f29_mul(f29_sub16(a, b), wv);
-                } else {
-                    const F29 bw = f29_mul(b, wv);
-                    lds[a0] = f29_reduce(f29_lazy2(a, bw));
-                    lds[a1] = f29_reduce(f29_sub16(a, bw));
-                }
-            }
-            __syncthreads();
-        }
+        tile_stages<DIF, LOGCW>(T, gm, p.tw, p.s0, p.logH, n_el);
         // ---- store
         const bool canon = p.canon != 0;
         for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
             uint32_t t, g, c;
-            split(e, t, g, c);
+            gm.split(e, t, g, c);
             if (c >= cw) continue;
-            base[(size_t)row_of(t, g) * p.w + c0 + c] = f29_store(lds[(((t << logG) + g) << LOGCW) + c], canon);
+            base[(size_t)gm.row_of(t, g) * p.w + c0 + c] = f29_store(T.get(gm.idx(t, g, c)), canon);
         }
     }
 }
@@ -237,6 +402,18 @@ __global__ __launch_bounds__(256) void k_to_f29limbs(const Fr* __restrict__ in, 
     out[3 * i] = make_uint4(v.l[0], v.l[1], v.l[2], v.l[3]);
     out[3 * i + 1] = make_uint4(v.l[4], v.l[5], v.l[6], v.l[7]);
     out[3 * i + 2] = make_uint4(v.l[8], 0u, 0u, 0u);
+}
+
+__global__ __launch_bounds__(256) void k_stage_twiddles(const Fr* __restrict__ pw, uint32_t logH,
+                                                         uint4* __restrict__ out) {
+    const size_t j = gtid();
+    if (j + 1 >= (1ull << logH)) return;
+    const uint32_t m = 64 - __clzll((unsigned long long)(j + 1));  // 2^(m-1) <= j + 1 < 2^m
+    const size_t i = j + 1 - (1ull << (m - 1));
+    const F29 v = f29_repack_in(f29_store(f29_from_fr(pw[i << (logH - m)]), true));
+    out[3 * j] = make_uint4(v.l[0], v.l[1], v.l[2], v.l[3]);
+    out[3 * j + 1] = make_uint4(v.l[4], v.l[5], v.l[6], v.l[7]);
+    out[3 * j + 2] = make_uint4(v.l[8], 0u, 0u, 0u);
 }
 
 __global__ __launch_bounds__(256) void k_pow_tables(const Fr* __restrict__ bases, size_t nbases, uint32_t L1,
@@ -277,46 +454,64 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
                       const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
                       hipStream_t st) {
     if (w == 0) return hipSuccess;
-    // column chunk: the power of two >= min(w, 8); CW * G = 8 (256-byte row runs)
-    uint32_t logCW = 0;
-    while ((1u << logCW) < w && logCW < 3) ++logCW;
-    const uint32_t CW = 1u << logCW;
-    const uint32_t logGmax = 3 - logCW;
-    const uint32_t nchunk = (uint32_t)((w + CW - 1) / CW);
-    // k <= 7: a tile of <= 1024 limb-form elements (36 KiB) plus the twist factors
-    const uint32_t kmax = 7;
+    // Tile = 2^k positions x G groups x CW columns = 1024 elements (36 KiB of
+    // LDS) where the array allows it, so every radix-4 group gives each of the
+    // 256 threads one quad.  Up to k = 10 stages per pass with one column per
+    // tile (2^19 points in 2 passes instead of 3: fewer HBM round trips); a
+    // pass with fewer stages takes the widest column chunk that still fits
+    // (k = 9: CW = 2, ..., k <= 7: CW = 8), and the narrow row accesses are
+    // merged in L2 by the XCD-aware tile order.  LSP_NTT_LOGCW (minimum column
+    // chunk) / LSP_NTT_KMAX override (LOGCW=3 KMAX=7: the r01 shape).
+    static const uint32_t logcw_env = [] {  // minimum log2 column chunk (bounds k)
+        const char* e = std::getenv("LSP_NTT_LOGCW");
+        return e ? (uint32_t)std::min(3, std::max(0, std::atoi(e))) : 0u;
+    }();
+    static const uint32_t kmax_env = [] {
+        const char* e = std::getenv("LSP_NTT_KMAX");
+        return e ? (uint32_t)std::min(10, std::max(1, std::atoi(e))) : 10u;
+    }();
+    uint32_t logCWmax = 0;  // the power of two >= min(w, 8)
+    while ((1u << logCWmax) < w && logCWmax < 3) ++logCWmax;
+    const uint32_t kmax = std::min(kmax_env, 10 - std::min(logCWmax, logcw_env));
     uint32_t ks[16], np;
-    auto run = [&](bool dif, uint32_t narr, const Fr* src, Fr* dst, const uint4* tw, int first_mode,
-                   bool canon_last) -> hipError_t {
-        plan_passes(logh, kmax, ks, np);
-        uint32_t s0 = 0;
-        for (uint32_t q = 0; q < np; ++q) {
-            const uint32_t k = ks[q];
-            const uint32_t logG = (logh - k) < logGmax ? (logh - k) : logGmax;
-            NttPass p;
-            p.src = src;
-            p.dst = dst;
-            p.tw = tw;
-            p.twist = twist;
-            p.L1 = L1;
-            p.L2 = L2;
-            p.twist_per_col = (uint32_t)twist_per_col;
-            p.logH = logh;
-            p.s0 = s0;
-            p.k = k;
-            p.logL = dif ? (logh - s0 - k) : s0;
-            p.logG = logG;
-            p.w = (uint32_t)w;
-            p.nchunk = nchunk;
-            p.canon = (canon_last && q + 1 == np) ? 1u : 0u;
-            p.narr = narr;
-            // the first forward pass loops over the cosets inside each workgroup
-            const uint64_t tiles = (uint64_t)(dif && q == 0 && first_mode == PASS_FWD_FIRST ? 1 : narr) *
-                                   ((1ull << logh) >> (k + logG)) * nchunk;
-            // tile, plus one twist factor per row in the first forward pass
-            const size_t lds = ((size_t(1) << (k + logG)) * CW + (size_t(1) << (k + logG))) * sizeof(F29);
-            const int mode = q == 0 ? first_mode : PASS_INPLACE;
-            const dim3 grid((unsigned)tiles), blk(256);
+    plan_passes(logh, kmax, ks, np);
+    // inverse: passes ks[0], ..., ks[np-1] (DIT, stages in increasing order);
+    // forward: ks[np-1], ..., ks[0] (DIF), so the forward's first pass covers
+    // the rows of the inverse's last pass and the two run as one (PASS_INV_FWD)
+    auto launch = [&](bool dif, int mode, uint32_t k, uint32_t s0, uint32_t narr, const Fr* src, Fr* dst,
+                      const uint4* tw, bool canon) -> hipError_t {
+        // widest column chunk the 1024-element tile allows at this k (CW = 1 at k = 10)
+        const uint32_t logCW = std::min(logCWmax, 10 - k);
+        const uint32_t CW = 1u << logCW;
+        const uint32_t nchunk = (uint32_t)((w + CW - 1) / CW);
+        const uint32_t want = k + logCW >= 10 ? 0u : 10 - k - logCW;
+        const uint32_t logG = std::min(logh - k, want);
+        NttPass p;
+        p.src = src;
+        p.dst = dst;
+        p.tw = tw;
+        p.tw_inv = tw_inv;
+        p.inv_gather = np == 1 ? 1u : 0u;
+        p.twist = twist;
+        p.L1 = L1;
+        p.L2 = L2;
+        p.twist_per_col = (uint32_t)twist_per_col;
+        p.logH = logh;
+        p.s0 = s0;
+        p.k = k;
+        p.logL = dif ? (logh - s0 - k) : s0;
+        p.logG = logG;
+        p.w = (uint32_t)w;
+        p.nchunk = nchunk;
+        p.canon = canon ? 1u : 0u;
+        p.narr = narr;
+        // the fused pass loops over the cosets inside each workgroup
+        const uint64_t tiles = (uint64_t)(mode == PASS_INV_FWD ? 1 : narr) * ((1ull << logh) >> (k + logG)) * nchunk;
+        // tile, plus one twist factor per row in the fused pass
+        const bool fac = mode == PASS_INV_FWD && !twist_per_col;
+        const size_t lds = ((size_t(1) << (k + logG)) * CW + (fac ? (size_t(1) << (k + logG)) : 0)) * sizeof(F29);
+        p.xcd = (tiles / nchunk) % 8 == 0 ? 1u : 0u;
+        const dim3 grid((unsigned)tiles), blk(256);
 #define LSP_NTT_LAUNCH(DIFV, MODEV)                                                                   \
     switch (logCW) {                                                                                  \
         case 0: hipLaunchKernelGGL((k_ntt_rm<DIFV, MODEV, 0>), grid, blk, lds, st, p); break;         \
@@ -324,39 +519,43 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
         case 2: hipLaunchKernelGGL((k_ntt_rm<DIFV, MODEV, 2>), grid, blk, lds, st, p); break;         \
         default: hipLaunchKernelGGL((k_ntt_rm<DIFV, MODEV, 3>), grid, blk, lds, st, p); break;        \
     }
-            if (dif) {
-                if (mode == PASS_FWD_FIRST) {
-                    LSP_NTT_LAUNCH(true, PASS_FWD_FIRST)
-                } else {
-                    LSP_NTT_LAUNCH(true, PASS_INPLACE)
-                }
-            } else {
-                if (mode == PASS_INV_FIRST) {
-                    LSP_NTT_LAUNCH(false, PASS_INV_FIRST)
-                } else {
-                    LSP_NTT_LAUNCH(false, PASS_INPLACE)
-                }
-            }
-#undef LSP_NTT_LAUNCH
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
-            s0 += k;
+        if (mode == PASS_INV_FWD) {
+            LSP_NTT_LAUNCH(true, PASS_INV_FWD)
+        } else if (dif) {
+            LSP_NTT_LAUNCH(true, PASS_INPLACE)
+        } else if (mode == PASS_INV_FIRST) {
+            LSP_NTT_LAUNCH(false, PASS_INV_FIRST)
+        } else {
+            LSP_NTT_LAUNCH(false, PASS_INPLACE)
         }
-        return hipSuccess;
+#undef LSP_NTT_LAUNCH
+        return hipGetLastError();
     };
     if (logh == 0) {
         // h = 1: the coefficient is the value; every coset row equals it
-        hipError_t e = hipMemcpyAsync(X, in, w * sizeof(Fr), hipMemcpyDeviceToDevice, st);
-        if (e != hipSuccess) return e;
         for (uint32_t k = 0; k < ncosets; ++k) {
-            e = hipMemcpyAsync(out + (size_t)k * w, X, w * sizeof(Fr), hipMemcpyDeviceToDevice, st);
+            hipError_t e = hipMemcpyAsync(out + (size_t)k * w, in, w * sizeof(Fr), hipMemcpyDeviceToDevice, st);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
     }
-    hipError_t e = run(false, 1, in, X, tw_inv, PASS_INV_FIRST, false);
+    uint32_t s0 = 0;
+    for (uint32_t q = 0; q + 1 < np; ++q) {  // inverse passes before the last
+        hipError_t e = launch(false, q == 0 ? PASS_INV_FIRST : PASS_INPLACE, ks[q], s0, 1, in, X, tw_inv, false);
+        if (e != hipSuccess) return e;
+        s0 += ks[q];
+    }
+    // the inverse's last stages + the forward's first ks[np-1] stages, per coset
+    hipError_t e = launch(true, PASS_INV_FWD, ks[np - 1], 0, ncosets, np == 1 ? in : X, out, tw_fwd, np == 1);
     if (e != hipSuccess) return e;
-    return run(true, ncosets, X, out, tw_fwd, PASS_FWD_FIRST, true);
+    s0 = ks[np - 1];
+    for (uint32_t q = 1; q < np; ++q) {  // the remaining forward passes
+        const uint32_t k = ks[np - 1 - q];
+        e = launch(true, PASS_INPLACE, k, s0, ncosets, out, out, tw_fwd, q + 1 == np);
+        if (e != hipSuccess) return e;
+        s0 += k;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_to_f29form(const Fr* in, Fr* out, size_t n, hipStream_t st) {
@@ -368,6 +567,13 @@ hipError_t launch_to_f29form(const Fr* in, Fr* out, size_t n, hipStream_t st) {
 hipError_t launch_to_f29limbs(const Fr* in, uint4* out, size_t n, hipStream_t st) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_to_f29limbs, dim3(nblocks(n, 256)), dim3(256), 0, st, in, out, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_stage_twiddles(const Fr* pw, uint32_t logH, uint4* out, hipStream_t st) {
+    const size_t n = (1ull << logH) - 1;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_stage_twiddles, dim3(nblocks(n, 256)), dim3(256), 0, st, pw, logH, out);
     return hipGetLastError();
 }
 

@@ -27,6 +27,9 @@ hipError_t launch_to_f29form(const Fr* in, Fr* out, size_t n, hipStream_t st);
 // the same, unpacked into 9 x 29-bit limbs padded to 48 bytes (3 x uint4 per
 // element): the NTT's twiddle tables, loaded with no repacking
 hipError_t launch_to_f29limbs(const Fr* in, uint4* out, size_t n, hipStream_t st);
+// stage-major twiddles for k_ntt_rm: entry 2^(m-1) - 1 + i = w_(2^m)^i (i < 2^(m-1),
+// m = 1..logH) from pw[x] = w_H^x (x < H/2), in the 48-byte 29-bit-limb slots
+hipError_t launch_stage_twiddles(const Fr* pw, uint32_t logH, uint4* out, hipStream_t st);
 // Two-level power tables: for each base b,
 // tab[b] = {b^j, j < 2^L1} ++ {b^(j 2^L1) * scale[b], j < 2^L2}   (scale nullable)
 hipError_t launch_pow_tables(const Fr* bases, size_t nbases, uint32_t L1, uint32_t L2, const Fr* scale,

@@ -262,8 +262,8 @@ def main_leg(args, dist, ranks_seen):
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": lde_traffic(args.log_n, w),
                          "valu_issue": valu_issue(["k_ntt_rm"]),
-                         "note": "VALU-bound: valu_issue = share of the chip's VALU issue cycles the NTT passes "
-                                 "use (PMC, profiles/*_valu_pmc.json); HBM frac is low by design",
+                         "note": "VALU-bound: valu_issue = share of SIMD cycles issuing VALU in the NTT passes "
+                                 "(PMC SQ_ACTIVE_INST_VALU, profiles/*_valu_pmc.json); HBM frac is low by design",
                          "algorithmic_bytes": lde_bytes, "ms": lde_ms},
             "roofline_valu": {"bound": "valu", "kernel": "trace Merkle tree (Poseidon2 leaf hash + levels)",
                               "achieved": valu_achieved, "unit": "M perm/s",
@@ -271,6 +271,18 @@ def main_leg(args, dist, ranks_seen):
                               "frac": valu_achieved / peak["mperm_per_s"] if peak else None,
                               "frac_at_measured_clock": (valu_achieved / peak["mperm_per_s_at_measured_clock"]
                                                          if peak else None),
+                              "impl_mad_floor": {
+                                  "mads_per_perm": peak["impl_mads_per_perm"] if peak else None,
+                                  "mperm_per_s": peak["impl_mad_floor_mperm_per_s"] if peak else None,
+                                  "frac": (valu_achieved / peak["impl_mad_floor_mperm_per_s"]
+                                           if peak and peak["impl_mad_floor_mperm_per_s"] else None),
+                                  "frac_at_measured_clock": (
+                                      valu_achieved / peak["impl_mad_floor_mperm_per_s_at_measured_clock"]
+                                      if peak and peak["impl_mad_floor_mperm_per_s_at_measured_clock"] else None),
+                                  "note": "the shipped multiplier's own MAD count (9 x 29-bit limbs, carry-free "
+                                          "columns) at the same MAD rate: the kernel's distance from its "
+                                          "instruction floor; the 128-MAD peak above is the 8 x 32-bit floor, whose "
+                                          "carry chains cost more than the extra MADs (DESIGN.md)"},
                               "peak_source": peak["source"] if peak else "profiles/r02_rates.json missing",
                               "fr_mul_achieved_g_per_s": valu_achieved * FR_MUL_PER_PERM / 1e3,
                               "fr_mul_peak_g_per_s": peak["gfrmul_per_s"] if peak else None,
@@ -453,18 +465,39 @@ def valu_peak():
     ghz_meas = r["peak_basis"]["measured_ghz"]
     mads = SIMDS * 64 / cyc * NOMINAL_GHZ * 1e9
     perm = mads / (MAD_PER_FR_MUL * FR_MUL_PER_PERM)
+    floor = impl_mads_per_perm()
     return {"mad_per_s": mads, "gfrmul_per_s": mads / MAD_PER_FR_MUL / 1e9, "mperm_per_s": perm / 1e6,
             "mperm_per_s_at_measured_clock": perm / 1e6 * ghz_meas / NOMINAL_GHZ,
+            "impl_mads_per_perm": floor,
+            "impl_mad_floor_mperm_per_s": mads / floor / 1e6 if floor else None,
+            "impl_mad_floor_mperm_per_s_at_measured_clock":
+                mads / floor / 1e6 * ghz_meas / NOMINAL_GHZ if floor else None,
             "source": f"profiles/r02_rates.json: v_mad_u64_u32 {cyc} cycles per wave64 per SIMD x {SIMDS} SIMDs "
                       f"at {NOMINAL_GHZ} GHz; {MAD_PER_FR_MUL} MADs per Fr product, {FR_MUL_PER_PERM} products "
                       f"per permutation (measured clock under MAD load {ghz_meas} GHz)"}
 
 
+def impl_mads_per_perm():
+    """v_mad_u64_u32 per permutation in the shipped multiplier, counted in the
+    generated asm (csrc/fr29_mul_gfx950_blk.inc: f29_mul_asm / f29_sqr_asm):
+    46 S-boxes x (3 squares + 2 products) for x^11 (rf = 8, rp = 22) -- the
+    instruction floor of this representation (9 x 29-bit limbs: 81 + 72 + 9
+    MADs per product, 45 + 72 + 9 per square), against which the kernel's
+    non-MAD overhead is measured."""
+    try:
+        src = open(os.path.join(ROOT, "linea_stark_prover_amd", "csrc", "fr29_mul_gfx950_blk.inc")).read()
+    except OSError:
+        return None
+    mul, sqr = src.split("f29_sqr_asm", 1) if "f29_sqr_asm" in src else (src, "")
+    nm, ns = mul.count("v_mad_u64_u32"), sqr.count("v_mad_u64_u32")
+    return (3 * 8 + 22) * (3 * ns + 2 * nm) if nm and ns else None
+
+
 def valu_issue(kernels):
-    """Time-weighted VALU issue utilisation of the named kernels from the
-    committed PMC passes (tools/pmc_valu.sh -> profiles/*_valu_pmc.json):
-    issue cycles (each instruction class at its measured cost,
-    profiles/r02_rates.json) / (1024 SIMDs x kernel cycles); None if absent."""
+    """Time-weighted VALU issue share of the named kernels from the committed
+    PMC passes (tools/pmc_valu.sh -> profiles/*_valu_pmc.json): SIMD cycles
+    with a VALU instruction issuing (SQ_ACTIVE_INST_VALU over all waves) /
+    (1024 SIMDs x kernel cycles); None if absent."""
     import glob
     d = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu_pmc.json"))):

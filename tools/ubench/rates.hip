@@ -142,6 +142,30 @@ template <int K> __global__ __launch_bounds__(256) void kr(Sample* out, unsigned
 #define MS(c) asm volatile("v_mad_u64_u32 %0, s[40:41], %1, %2, %0" : "+v"(c) : "v"(a), "s"(seed) : "s40", "s41")
             MS(c0); MS(c1); MS(c2); MS(c3); MS(c4); MS(c5); MS(c6); MS(c7);
 #undef MS
+        } else if (K == 28) {  // v_mad_u64_u32 and v_fma_f64 interleaved: separate pipes?
+#define MF(c, dd) asm volatile("v_mad_u64_u32 %0, s[40:41], %2, %3, %0\n\tv_fma_f64 %1, %4, %5, %1" : "+v"(c), "+v"(dd) : "v"(a), "v"(b), "v"(dk0), "v"(dk1) : "s40", "s41")
+            MF(c0, d0); MF(c1, d1); MF(c2, d2); MF(c3, d3);
+#undef MF
+        } else if (K == 29) {  // v_mad_u64_u32 and v_pk_fma_f32 interleaved
+#define MP(c, dd) asm volatile("v_mad_u64_u32 %0, s[40:41], %2, %3, %0\n\tv_pk_fma_f32 %1, %4, %5, %1" : "+v"(c), "+v"(dd) : "v"(a), "v"(b), "v"(dk0), "v"(dk1) : "s40", "s41")
+            MP(c0, d0); MP(c1, d1); MP(c2, d2); MP(c3, d3);
+#undef MP
+        } else if (K == 30) {  // v_mad_u64_u32 and v_mad_u32_u24 interleaved
+#define M24(c, x) asm volatile("v_mad_u64_u32 %0, s[40:41], %2, %3, %0\n\tv_mad_u32_u24 %1, %1, %3, %1" : "+v"(c), "+v"(x) : "v"(a), "v"(b) : "s40", "s41")
+            M24(c0, u0); M24(c1, u1); M24(c2, u2); M24(c3, u3);
+#undef M24
+        } else if (K == 31) {  // v_mad_u64_u32 and v_lshrrev_b64 interleaved
+#define ML(c, cc) asm volatile("v_mad_u64_u32 %0, s[40:41], %2, %3, %0\n\tv_lshrrev_b64 %1, 29, %1" : "+v"(c), "+v"(cc) : "v"(a), "v"(b) : "s40", "s41")
+            ML(c0, c4); ML(c1, c5); ML(c2, c6); ML(c3, c7);
+#undef ML
+        } else if (K == 32) {  // v_fma_f64 and v_add_u32 interleaved
+#define FA(dd, x) asm volatile("v_fma_f64 %0, %2, %3, %0\n\tv_add_u32 %1, %1, %4" : "+v"(dd), "+v"(x) : "v"(dk0), "v"(dk1), "v"(b))
+            FA(d0, u0); FA(d1, u1); FA(d2, u2); FA(d3, u3);
+#undef FA
+        } else if (K == 33) {  // v_mul_hi_u32 and v_mul_lo_u32 interleaved (32-bit multiplier)
+#define HL(x, y) asm volatile("v_mul_hi_u32 %0, %0, %2\n\tv_mul_lo_u32 %1, %1, %2" : "+v"(x), "+v"(y) : "v"(b))
+            HL(u0, u1); HL(u2, u3); HL(u4, u5); HL(u6, u7);
+#undef HL
         } else if (K == 17) {  // v_sub_u32 chains on a 64-bit pair: v_sub_co_u32 / v_subb_co_u32 (8 instructions)
 #define SB(x, y) asm volatile("v_sub_co_u32 %0, vcc, %0, %2\n\tv_subb_co_u32 %1, vcc, %1, %2, vcc" : "+v"(x), "+v"(y) : "v"(a) : "vcc")
             SB(u0, u1); SB(u2, u3); SB(u4, u5); SB(u6, u7);
@@ -224,6 +248,12 @@ int main(int argc, char** argv) {
     rows.push_back(run<23>("v_mad_u64_u32 + v_add_u32 (1:1)", out, sink, cus));
     rows.push_back(run<25>("v_mad_u64_u32 (x inline 1)", out, sink, cus));
     rows.push_back(run<27>("v_mad_u64_u32 (x SGPR)", out, sink, cus));
+    rows.push_back(run<28>("v_mad_u64_u32 + v_fma_f64 (1:1)", out, sink, cus));
+    rows.push_back(run<29>("v_mad_u64_u32 + v_pk_fma_f32 (1:1)", out, sink, cus));
+    rows.push_back(run<30>("v_mad_u64_u32 + v_mad_u32_u24 (1:1)", out, sink, cus));
+    rows.push_back(run<31>("v_mad_u64_u32 + v_lshrrev_b64 (1:1)", out, sink, cus));
+    rows.push_back(run<32>("v_fma_f64 + v_add_u32 (1:1)", out, sink, cus));
+    rows.push_back(run<33>("v_mul_hi_u32 + v_mul_lo_u32 (1:1)", out, sink, cus));
     printf("device %s, %d CUs; cycles per wave64 instruction per SIMD (shader clock, s_memtime), "
            "median over waves; GHz = s_memtime / s_memrealtime\n", pr.gcnArchName, cus);
     printf("%-34s %21s   %27s   %s\n", "", "per-wave median", "whole-grid span", "");

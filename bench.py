@@ -20,6 +20,9 @@ Legs (rank 0 prints ONE JSON line):
                  all rows / max-over-ranks wall time ("scaling": "weak").
                  ``--shard`` instead proves ONE trace over the N ranks
                  (lsp_prove_sharded, "scaling": "strong").
+  batch          BASELINE configs[4] (configs[1] at N = 1): every rank proves
+                 its own 2^22-row trace (device-generated); all rows / the
+                 slowest rank's time (--batch-leg).
   sharded        C4 (BASELINE configs[3]): one 2^24-row proof
                  sharded over all N ranks (rank g owns LDE rows
                  [g N/G, (g+1) N/G)), exchanging subtree roots, quotient
@@ -93,6 +96,10 @@ def parse(argv=None):
     ap.add_argument("--shard-timeout", type=float, default=900.0,
                     help="seconds before a rank's watchdog abandons the sharded leg")
     ap.add_argument("--no-host-trace-leg", action="store_true")
+    ap.add_argument("--batch-leg", default="22",
+                    help="log_n list of the batch leg (BASELINE configs[4]: one independent 2^22 proof per "
+                         "GPU; at N = 1 configs[1]); 'none' to skip")
+    ap.add_argument("--batch-leg-steps", type=int, default=2)
     ap.add_argument("--device", type=int, default=None, help="GPU of this rank (default: LOCAL_RANK mod #GPUs)")
     ap.add_argument("--dump-proof", default=None, help="rank 0 writes the last proof here")
     ap.add_argument("--inflight", type=int, default=3,
@@ -146,6 +153,15 @@ def main():
     if args.shard or (shard_sizes and world > 1):
         from linea_stark_prover_amd import shard as S  # noqa: F401  (torch before the HIP library)
     out, ctx = main_leg(args, dist, ranks_seen)
+    batch_sizes = [] if args.batch_leg == "none" or args.shard or args.air != "perm" else \
+        [int(x) for x in args.batch_leg.split(",") if x]
+    if batch_sizes:
+        try:
+            batch = batch_leg(args, dist, ctx, batch_sizes)
+        except Exception as e:  # the main line is still reported
+            batch = {"error": f"{type(e).__name__}: {e}"}
+        if rank == 0:
+            out["batch"] = batch
     if shard_sizes:
         sharded = guarded_shard_leg(args, dist, ctx, shard_sizes, out)
         if rank == 0:
@@ -321,6 +337,38 @@ def host_trace_leg(args, ctx, trace, air, pub):
     return {"mean": sum(ts) / len(ts), "median": statistics.median(ts), "steps": len(ts),
             "trace_bytes": int(trace.nbytes),
             "note": "the trace starts in pageable host memory each step; value above starts with it in HBM"}
+
+
+def batch_leg(args, dist, ctx, sizes):
+    """BASELINE configs[4] (and configs[1] at N = 1): every rank proves its own
+    independent 2^log_n trace (device-generated, rank-seeded), no data-path
+    collective; value = all rows / the slowest rank's time (weak scaling)."""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import StarkConfig
+    from linea_stark_prover_amd.replicas import rank_seed, timed_steps
+    import numpy as np
+    cfg = StarkConfig(seed=args.seed)
+    a, d, _ = cfg.seeded()
+    pub = np.concatenate([a, d])
+    air = permutation_air(args.ncols)
+    w = 2 * args.ncols + 2
+    runs = []
+    for log_n in sizes:
+        h = 1 << log_n
+        dtrace = ctx.gen_permutation_trace_device(log_n, args.ncols, a, d, seed=rank_seed(args.seed, dist.rank))
+        step = lambda: ctx.prove(dtrace, air, pub, h, w)  # noqa: E731
+        elapsed, proof = timed_steps(step, args.batch_leg_steps, 1, dist, sync=ctx.synchronize)
+        ctx.dev_free(dtrace)
+        run = {"log_n": log_n, "rows_per_rank": h, "steps": args.batch_leg_steps, "warmup": 1,
+               "prove_time_s": elapsed / args.batch_leg_steps,
+               "value": dist.world * h * args.batch_leg_steps / elapsed, "unit": "trace-rows/s",
+               "scaling": "weak",
+               "workload": f"{args.ncols}x{args.ncols} permutation AIR, one independent 2^{log_n}-row proof per "
+                           f"rank ({dist.world} rank(s))"}
+        if dist.rank == 0:
+            run["verified"] = bool(ctx.verify(proof, air, pub))
+        runs.append(run)
+    return {"runs": runs}
 
 
 def shard_leg_sizes(args, world):

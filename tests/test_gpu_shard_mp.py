@@ -66,7 +66,7 @@ def test_bench_gpus2_shard_spawns_ranks():
     """bench.py --gpus 2 started without a launcher runs two
     ranks (here both on the box's one GPU over gloo) and reports n_gpus 2"""
     o = _bench_json(["--gpus", "2", "--shard", "--comm", "gloo", "--log-n", "12", "--steps", "1", "--warmup", "1",
-                     "--no-cpu-baseline", "--shard-leg", "none"])
+                     "--no-cpu-baseline", "--shard-leg", "none", "--batch-leg", "none"])
     assert o["n_gpus"] == 2 and o["n_ranks_seen"] == 2 and o["verified"] is True
     assert o["scaling"] == "strong"
 
@@ -75,8 +75,11 @@ def test_bench_sharded_leg_two_ranks():
     """the C4 'sharded' field: one device-generated trace proved by two ranks
     (gloo, sharing one GPU) verifies; the replicas value beside it is weak scaling"""
     o = _bench_json(["--gpus", "2", "--log-n", "10", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
-                     "--shard-leg", "12,13", "--shard-leg-steps", "1", "--shard-leg-warmup", "0"])
+                     "--shard-leg", "12,13", "--shard-leg-steps", "1", "--shard-leg-warmup", "0",
+                     "--batch-leg", "11", "--batch-leg-steps", "1"])
     assert o["n_gpus"] == 2 and o["scaling"] == "weak" and o["verified"] is True
+    b = o["batch"]["runs"][0]  # configs[4]'s shape: one independent proof per rank
+    assert b["log_n"] == 11 and b["verified"] is True and b["scaling"] == "weak"
     sh = o["sharded"]
     assert sh["comm"] == "gloo" and sh["n_ranks_seen"] == 2, sh
     assert [r["log_n"] for r in sh["runs"]] == [12, 13]
@@ -87,7 +90,7 @@ def test_bench_sharded_leg_single_gpu_equals_prove():
     """N = 1: the sharded field is lsp_prove itself (prove_shard over SoloComm),
     and the device-generated trace proves and verifies"""
     o = _bench_json(["--log-n", "10", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--inflight", "0",
-                     "--shard-leg", "14", "--shard-leg-steps", "2"])
+                     "--shard-leg", "14", "--shard-leg-steps", "2", "--batch-leg", "none"])
     sh = o["sharded"]
     assert sh["comm"] == "solo" and sh["n_ranks_seen"] == 1
     assert sh["runs"][0]["verified"] is True

@@ -1,9 +1,9 @@
 // Exchange layer of the sharded prover.  A proof over G ranks
 // needs only two collectives, both on device buffers and both small except
-// the quotient-chunk exchange: allgather (subtree roots, quotient chunks,
-// the FRI vector once it is short, query openings) and broadcast (opened
-// values from rank 0).  The transcript runs redundantly on every rank, so
-// no challenge is ever sent.
+// the quotient-chunk exchange: allgather (subtree roots, the FRI vector once
+// it is short, query openings) and broadcast (the quotient chunks, one
+// broadcast per holding rank; opened values from rank 0).  The transcript
+// runs redundantly on every rank, so no challenge is ever sent.
 //
 //   SoloComm     G = 1 (the single-GPU prover; allgather is a copy)
 //   ThreadComm   G ranks of one process, one thread and one lsp_ctx each:

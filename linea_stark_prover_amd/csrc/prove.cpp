@@ -487,7 +487,9 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         const Fr wh = host_two_adic_generator(log_h);
         const Fr wh_inv = host_inv_cached(wh);
         Fr* qv = ctx->fbuf("q_values", Q);  // the h x q chunk matrix, on every rank
-        Fr* qloc = G == 1 ? qv : ctx->fbuf("q_local", Sq);
+        // ranks g < Gq evaluate points straight into their slot of the exchange buffer
+        Fr* stage = G == 1 ? nullptr : ctx->fbuf("q_stage", Sq * Gq);
+        Fr* qloc = G == 1 ? qv : (g < Gq ? stage + (size_t)g * Sq : nullptr);
         std::vector<Fr> zh(q), izh(q);
         if (row0 < Q) {
             const uint64_t i0 = host_bitrev(g, logGq);
@@ -544,9 +546,9 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             LSP_HIP(launch_quotient(qa, st));
         }
         if (G > 1) {
-            // rank r < Gq holds chunks j = bitrev(r) + Gq c as an h x cpr matrix
-            Fr* stage = ctx->fbuf("q_stage", Sq * G);
-            comm.allgather(ctx, qloc, stage, Sq * sizeof(Fr));
+            // rank r < Gq holds chunks j = bitrev(r) + Gq c as an h x cpr matrix: one
+            // broadcast per holder (only the Gq holders send: Gq/G of an allgather's bytes)
+            for (uint32_t r = 0; r < Gq; ++r) comm.bcast(ctx, stage + (size_t)r * Sq, Sq * sizeof(Fr), (int)r);
             LSP_HIP(launch_assemble_chunks(stage, logGq, cpr, h, qv, st));
         }
         T.end("compute quotient polynomial");

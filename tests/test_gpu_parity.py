@@ -38,8 +38,11 @@ def c_ptr(a):
 
 
 # ------------------------------------------------------------------ LDE
+# pass plans (k_ntt.hip, k <= 10 per pass): one fused pass up to 2^10; [6,5] [6,6] [7,6]
+# [7,7] [8,7] [8,8] [9,8] [9,9] above, with the per-pass column chunk and partial chunks
 @pytest.mark.parametrize("logh,w,added", [(1, 1, 1), (3, 2, 3), (5, 8, 3), (8, 14, 3), (10, 4, 2), (12, 8, 3),
-                                          (13, 3, 3), (11, 1, 3)])
+                                          (13, 3, 3), (11, 1, 3), (14, 5, 3), (15, 14, 3), (16, 2, 1),
+                                          (17, 1, 3), (18, 3, 2)])
 def test_coset_lde_matches_oracle(gpu_ctx, oracle_lib, logh, w, added):
     rng = np.random.default_rng(logh * 100 + w)
     h = 1 << logh

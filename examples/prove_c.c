@@ -97,6 +97,21 @@ int main(int argc, char** argv) {
     uint8_t* bytes = (uint8_t*)malloc(len);
     CHECK(lsp_proof_serialize(proof, bytes, len, &len), ctx);
     const int ok = lsp_verify(ctx, air, k, pub, 2, bytes, len);
+    /* the proof as p3_uni_stark::Proof<SC> fields (lsp_proof_view) and back to the same bytes */
+    lsp_proof_view view;
+    CHECK(lsp_proof_get_view(proof, &view), ctx);
+    lsp_proof* rebuilt = NULL;
+    CHECK(lsp_proof_from_view(&view, &rebuilt), ctx);
+    size_t len2 = 0;
+    CHECK(lsp_proof_serialize(rebuilt, NULL, 0, &len2), ctx);
+    uint8_t* bytes2 = (uint8_t*)malloc(len2);
+    CHECK(lsp_proof_serialize(rebuilt, bytes2, len2, &len2), ctx);
+    const int same = len2 == len && memcmp(bytes, bytes2, len) == 0;
+    printf("proof view: degree_bits %u, width %u, %u quotient chunks, %u queries, %u FRI rounds, paths %u; "
+           "rebuilt bytes %s\n", view.degree_bits, view.width, 1u << view.log_quotient_chunks, view.num_queries,
+           view.num_fri_rounds, view.input_path_len, same ? "identical" : "DIFFER");
+    lsp_proof_free(rebuilt);
+    free(bytes2);
     bytes[len / 2] ^= 1;
     const int bad = lsp_verify(ctx, air, k, pub, 2, bytes, len);
     printf("2^%u rows: proof %zu bytes, verify %s, tampered %s\n", log_n, len, ok == LSP_OK ? "ok" : "FAILED",
@@ -105,5 +120,5 @@ int main(int argc, char** argv) {
     lsp_ctx_destroy(ctx);
     free(bytes);
     free(trace);
-    return (ok == LSP_OK && bad != LSP_OK) ? 0 : 1;
+    return (ok == LSP_OK && bad != LSP_OK && same) ? 0 : 1;
 }

@@ -34,4 +34,4 @@ def test_c_program_proves_and_verifies(product_lib, tmp_path):
     exe = _build(tmp_path)
     r = subprocess.run([exe, "12"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "verify ok, tampered rejected" in r.stdout
+    assert "verify ok, tampered rejected" in r.stdout and "rebuilt bytes identical" in r.stdout

@@ -183,6 +183,58 @@ __device__ __forceinline__ F29 f29_reduce(const F29& a) {
     return o;
 }
 
+// v - q r as f29_reduce, with q r taken from a per-workgroup LDS table
+// (f29_qtab_init) instead of 64-bit multiply-and-shift chains: 3 plain 32-bit
+// ops per limb instead of ~5 (two of them 64-bit), about half the VALU cycles.
+// Entries hold biased limbs so every partial sum stays in [0, 2^32) and the
+// carries are logical shifts: T_0 = 2^30 - Q_0, T_i = 2^30 - 2 - Q_i
+// (i = 1..7), T_8 = -2 - Q_8 (mod 2^32) for Q = q r in normalised limbs; the
+// running carry (s_i >> 29) is the true carry + 2, which the next entry's -2
+// cancels.  Valid for values < 64 r (q <= 63) with limbs < 2.41 2^30; result
+// normalised and < 2 r (the same value f29_reduce returns).
+constexpr uint32_t F29_QTAB_N = 64;
+
+// fill the table (F29_QTAB_N entries of 3 x uint4: limbs 0-3, 4-7, 8); the
+// caller's next __syncthreads publishes it
+__device__ __forceinline__ void f29_qtab_init(uint4* t) {
+    for (uint32_t q = threadIdx.x; q < F29_QTAB_N; q += blockDim.x) {
+        uint32_t Q[9];
+        uint64_t c = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint64_t v = (uint64_t)q * p29(i) + c;
+            Q[i] = (uint32_t)v & F29_MASK;
+            c = v >> 29;
+        }
+        Q[8] = (uint32_t)((uint64_t)q * p29(8) + c);
+        uint32_t T[9];
+        T[0] = (1u << 30) - Q[0];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) T[i] = (1u << 30) - 2u - Q[i];
+        T[8] = 0u - 2u - Q[8];
+        t[3 * q] = make_uint4(T[0], T[1], T[2], T[3]);
+        t[3 * q + 1] = make_uint4(T[4], T[5], T[6], T[7]);
+        t[3 * q + 2] = make_uint4(T[8], 0u, 0u, 0u);
+    }
+}
+
+__device__ __forceinline__ F29 f29_reduce_qt(const F29& a, const uint4* __restrict__ t) {
+    const uint32_t q = __umulhi(a.l[8], 0xdb651d12u) >> 20;  // as f29_reduce
+    const uint4 x = t[3 * q], y = t[3 * q + 1];
+    const uint32_t z = reinterpret_cast<const uint32_t*>(t + 3 * q + 2)[0];
+    const uint32_t T[9] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z};
+    F29 o;
+    uint32_t k = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint32_t s = a.l[i] + T[i] + k;
+        o.l[i] = s & F29_MASK;
+        k = s >> 29;
+    }
+    o.l[8] = a.l[8] + T[8] + k;
+    return o;
+}
+
 __device__ __forceinline__ F29 f29_zero() {
     F29 z;
 #pragma unroll

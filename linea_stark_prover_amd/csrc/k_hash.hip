@@ -17,14 +17,23 @@
 
 namespace lsp {
 
+// waves per SIMD requested for the one-row-per-lane leaf kernels (the LDS
+// reduction table lets the compiler hoist loads and grow to 3 waves)
+#ifndef LSP_P2_ROWS_WPE
+#define LSP_P2_ROWS_WPE 1
+#endif
+
 namespace {
 template <uint32_t D>
 __global__ __launch_bounds__(256) void k_permute(Fr* __restrict__ st, size_t n, const F29* __restrict__ rc,
                                                  uint32_t rf, uint32_t rp) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
+    f29_qtab_init(qt);
+    __syncthreads();
     const size_t i = gtid();
     if (i >= n) return;
     F29 s0 = f29_from_fr(st[3 * i]), s1 = f29_from_fr(st[3 * i + 1]), s2 = f29_from_fr(st[3 * i + 2]);
-    permute3_f29<D>(s0, s1, s2, rc, rf, rp);
+    permute3_f29<D>(s0, s1, s2, rc, rf, rp, qt);
     st[3 * i] = f29_to_fr(s0);
     st[3 * i + 1] = f29_to_fr(s1);
     st[3 * i + 2] = f29_to_fr(s2);
@@ -33,19 +42,25 @@ __global__ __launch_bounds__(256) void k_permute(Fr* __restrict__ st, size_t n, 
 // COOP: one row per DPP quad (poseidon2_f29.hpp), for batches narrower than
 // the chip; otherwise one row per lane.
 template <uint32_t D, bool COOP>
-__global__ __launch_bounds__(256) void k_hash_rows1(const Fr* __restrict__ m, uint32_t w, size_t nrows,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSP_P2_ROWS_WPE))) void k_hash_rows1(const Fr* __restrict__ m, uint32_t w, size_t nrows,
                                                     Fr* __restrict__ out, const F29* __restrict__ rc, uint32_t rf,
                                                     uint32_t rp) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
+    f29_qtab_init(qt);
+    __syncthreads();
     const size_t i = COOP ? (gtid() >> 2) : gtid();
     if (i >= nrows) return;
     const Fr* row = m + i * w;
-    const Fr d = sponge_f29<D, COOP>([&](uint32_t k) { return row[k]; }, w, rc, rf, rp);
+    const Fr d = sponge_f29<D, COOP>([&](uint32_t k) { return row[k]; }, w, rc, rf, rp, qt);
     if (!COOP || (threadIdx.x & 3) == 0) out[i] = d;
 }
 
 template <uint32_t D, bool COOP>
-__global__ __launch_bounds__(256) void k_hash_rows_multi(MatList ml, size_t nrows, Fr* __restrict__ out,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSP_P2_ROWS_WPE))) void k_hash_rows_multi(MatList ml, size_t nrows, Fr* __restrict__ out,
                                                          const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
+    f29_qtab_init(qt);
+    __syncthreads();
     const size_t i = COOP ? (gtid() >> 2) : gtid();
     if (i >= nrows) return;
     uint32_t total = 0;
@@ -58,13 +73,16 @@ __global__ __launch_bounds__(256) void k_hash_rows_multi(MatList ml, size_t nrow
         }
         return ml.ptr[j][i * ml.width[j] + k];
     };
-    const Fr d = sponge_f29<D, COOP>(get, total, rc, rf, rp);
+    const Fr d = sponge_f29<D, COOP>(get, total, rc, rf, rp, qt);
     if (!COOP || (threadIdx.x & 3) == 0) out[i] = d;
 }
 
 template <uint32_t D, bool COOP>
 __global__ __launch_bounds__(256) void k_fold_hash(FoldSpec f, size_t nleaves, Fr* __restrict__ out,
                                                    const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
+    f29_qtab_init(qt);
+    __syncthreads();
     const size_t j = COOP ? (gtid() >> 2) : gtid();
     if (j >= nleaves) return;
     Fr e[2];
@@ -78,16 +96,19 @@ __global__ __launch_bounds__(256) void k_fold_hash(FoldSpec f, size_t nleaves, F
         f.vout[2 * j] = e[0];
         f.vout[2 * j + 1] = e[1];
     }
-    const Fr d = sponge_f29<D, COOP>([&](uint32_t k) { return e[k]; }, 2, rc, rf, rp);
+    const Fr d = sponge_f29<D, COOP>([&](uint32_t k) { return e[k]; }, 2, rc, rf, rp, qt);
     if (!COOP || (threadIdx.x & 3) == 0) out[j] = d;
 }
 
 template <uint32_t D, bool COOP>
 __global__ __launch_bounds__(256) void k_merkle_level(const Fr* __restrict__ src, Fr* __restrict__ dst, size_t nout,
                                                       const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
+    f29_qtab_init(qt);
+    __syncthreads();
     const size_t i = COOP ? (gtid() >> 2) : gtid();
     if (i >= nout) return;
-    const Fr d = compress_f29<D, COOP>(src[2 * i], src[2 * i + 1], rc, rf, rp);
+    const Fr d = compress_f29<D, COOP>(src[2 * i], src[2 * i + 1], rc, rf, rp, qt);
     if (!COOP || (threadIdx.x & 3) == 0) dst[i] = d;
 }
 
@@ -97,6 +118,9 @@ __global__ __launch_bounds__(256) void k_merkle_level(const Fr* __restrict__ src
 template <uint32_t D>
 __global__ __launch_bounds__(256) void k_merkle_top(Fr* __restrict__ layers, size_t off, uint32_t len,
                                                     const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
+    f29_qtab_init(qt);
+    __syncthreads();
     __shared__ Fr buf[128];
     for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) buf[e] = layers[off + e];
     __syncthreads();
@@ -106,7 +130,7 @@ __global__ __launch_bounds__(256) void k_merkle_top(Fr* __restrict__ layers, siz
     while (len > 1) {
         const uint32_t nout = len / 2;
         Fr r;
-        if (q < nout) r = compress_f29<D, true>(buf[2 * q], buf[2 * q + 1], rc, rf, rp);
+        if (q < nout) r = compress_f29<D, true>(buf[2 * q], buf[2 * q + 1], rc, rf, rp, qt);
         __syncthreads();
         if (q < nout && lead) {
             buf[q] = r;
@@ -126,6 +150,9 @@ template <uint32_t D>
 __global__ __launch_bounds__(256) void k_grind(Fr pre0, Fr pre1, Fr pre2, uint32_t wlane, uint64_t base,
                                                uint64_t count, uint32_t bits, const F29* __restrict__ rc,
                                                uint32_t rf, uint32_t rp, unsigned long long* __restrict__ best) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
+    f29_qtab_init(qt);
+    __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const F29 c0 = f29_from_fr(pre0), c1 = f29_from_fr(pre1), c2 = f29_from_fr(pre2);
     const uint64_t mask = bits >= 64 ? ~0ull : ((1ull << bits) - 1);
@@ -133,7 +160,7 @@ __global__ __launch_bounds__(256) void k_grind(Fr pre0, Fr pre1, Fr pre2, uint32
         const uint64_t w = base + i;
         const F29 fw = f29_from_fr(fr_from_u64(w));
         F29 s0 = wlane == 0 ? fw : c0, s1 = wlane == 0 ? c1 : fw, s2 = c2;
-        permute3_f29<D>(s0, s1, s2, rc, rf, rp);
+        permute3_f29<D>(s0, s1, s2, rc, rf, rp, qt);
         const Fr c = fr_to_canonical(f29_to_fr(s0));
         const uint64_t lo = (uint64_t)c.v[0] | ((uint64_t)c.v[1] << 32);
         if ((lo & mask) == 0) atomicMin(best, (unsigned long long)w);
@@ -145,9 +172,12 @@ __global__ __launch_bounds__(256) void k_grind(Fr pre0, Fr pre1, Fr pre2, uint32
 template <uint32_t D>
 __global__ __launch_bounds__(256) void k_calib_perm(Fr* __restrict__ out, uint32_t iters, const F29* __restrict__ rc,
                                                     uint32_t rf, uint32_t rp) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
+    f29_qtab_init(qt);
+    __syncthreads();
     const size_t t = gtid();
     F29 s0 = f29_from_fr(fr_from_u64(t + 1)), s1 = f29_from_fr(fr_from_u64(3 * t + 7)), s2 = f29_zero();
-    for (uint32_t i = 0; i < iters; ++i) permute3_f29<D>(s0, s1, s2, rc, rf, rp);
+    for (uint32_t i = 0; i < iters; ++i) permute3_f29<D>(s0, s1, s2, rc, rf, rp, qt);
     out[t] = f29_to_fr(s0);
 }
 

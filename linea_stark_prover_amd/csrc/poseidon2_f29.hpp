@@ -9,9 +9,10 @@
 //     folded into the next S-box input with the round constant: inputs
 //     < 4 Y + 2 inside a permutation (Y = the S-box output bound), < 8 Y + 6
 //     at the start of a sponge permutation (s2 carries over);
-//   partial rounds: t = reduce(s0 + s1 + s2) < 2 r, s2 = reduce(2 s2 + t)
-//     (limb-wise sums into f29_reduce, which normalises limbs < 2^32),
-//     s1 grows by < 2 r per round and is reduced after the partial rounds;
+//   partial rounds: u = reduce(y + s1 + s2) < 2 r, s1 = reduce(s1 + u),
+//     s2 = reduce(2 s2 + u): limb-wise sums (< 13.7 r, limbs < 1.5 2^30)
+//     into the LDS-table reduction f29_reduce_qt (`qt`, valid below 64 r),
+//     so s1 and s2 stay < 2 r for any number of partial rounds;
 //   the output state is normalised and < 4 Y.
 #pragma once
 #include "fr29.hpp"
@@ -31,7 +32,7 @@ __device__ __forceinline__ F29 sbox29(const F29& x) {
 // [rf/2][3], terminal external [rf/2][3], internal [rp])
 template <uint32_t D>
 __device__ __forceinline__ void permute3_f29(F29& s0, F29& s1, F29& s2, const F29* __restrict__ rc29, uint32_t rf,
-                                             uint32_t rp) {
+                                             uint32_t rp, const uint4* __restrict__ qt) {
     const uint32_t half = rf / 2;
     const F29* ini = rc29;
     const F29* ter = rc29 + 3 * half;
@@ -46,17 +47,16 @@ __device__ __forceinline__ void permute3_f29(F29& s0, F29& s1, F29& s2, const F2
     }
     // x: the next partial-round S-box input (s0 + round constant)
     F29 x = rp ? f29_add(f29_lazy2(s0, itl[0]), t) : f29_add(s0, t);
-    s1 = f29_reduce(f29_lazy2(s1, t));
-    s2 = f29_reduce(f29_lazy2(s2, t));
+    s1 = f29_reduce_qt(f29_lazy2(s1, t), qt);  // < 38.8 r, limbs < 2^31
+    s2 = f29_reduce_qt(f29_lazy2(s2, t), qt);
     for (uint32_t r = 0; r < rp; ++r) {
         const F29 y = sbox29<D>(x);
-        const F29 u = f29_reduce(f29_lazy3(y, s1, s2));
-        s1 = f29_add(s1, u);
-        s2 = f29_reduce(f29_lazy3(s2, s2, u));
+        const F29 u = f29_reduce_qt(f29_lazy3(y, s1, s2), qt);  // < 13.7 r
+        s1 = f29_reduce_qt(f29_lazy2(s1, u), qt);
+        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);
         x = r + 1 < rp ? f29_add(f29_lazy2(y, itl[r + 1]), u) : f29_add(y, u);
     }
     s0 = x;
-    s1 = f29_reduce(s1);
     t = f29_zero();
     for (uint32_t r = 0; r < half; ++r) {
         s0 = sbox29<D>(f29_add(f29_lazy2(s0, ter[3 * r + 0]), t));
@@ -134,7 +134,7 @@ __device__ __forceinline__ F29 sbox29_coop(const F29& x) {
 
 template <uint32_t D>
 __device__ __forceinline__ void permute3_f29_coop(F29& s0, F29& s1, F29& s2, const F29* __restrict__ rc29,
-                                                  uint32_t rf, uint32_t rp) {
+                                                  uint32_t rf, uint32_t rp, const uint4* __restrict__ qt) {
     const uint32_t j = min(threadIdx.x & 3u, 2u);
     const uint32_t half = rf / 2;
     const F29* ini = rc29;
@@ -143,17 +143,16 @@ __device__ __forceinline__ void permute3_f29_coop(F29& s0, F29& s1, F29& s2, con
     F29 t = f29_lazy3(s0, s1, s2);
     for (uint32_t r = 0; r < half; ++r) t = full_round_coop<D>(s0, s1, s2, t, ini + 3 * r, j);
     F29 x = rp ? f29_add(f29_lazy2(s0, itl[0]), t) : f29_add(s0, t);
-    s1 = f29_reduce(f29_lazy2(s1, t));
-    s2 = f29_reduce(f29_lazy2(s2, t));
+    s1 = f29_reduce_qt(f29_lazy2(s1, t), qt);  // < 38.8 r, limbs < 2^31
+    s2 = f29_reduce_qt(f29_lazy2(s2, t), qt);
     for (uint32_t r = 0; r < rp; ++r) {
         const F29 y = sbox29_coop<D>(x);
-        const F29 u = f29_reduce(f29_lazy3(y, s1, s2));
-        s1 = f29_add(s1, u);
-        s2 = f29_reduce(f29_lazy3(s2, s2, u));
+        const F29 u = f29_reduce_qt(f29_lazy3(y, s1, s2), qt);  // < 13.7 r
+        s1 = f29_reduce_qt(f29_lazy2(s1, u), qt);
+        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);
         x = r + 1 < rp ? f29_add(f29_lazy2(y, itl[r + 1]), u) : f29_add(y, u);
     }
     s0 = x;
-    s1 = f29_reduce(s1);
     t = f29_zero();
     for (uint32_t r = 0; r < half; ++r) t = full_round_coop<D>(s0, s1, s2, t, ter + 3 * r, j);
     s0 = f29_add(s0, t);
@@ -163,17 +162,18 @@ __device__ __forceinline__ void permute3_f29_coop(F29& s0, F29& s1, F29& s2, con
 
 template <uint32_t D, bool COOP = false>
 __device__ __forceinline__ void permute3_any(F29& s0, F29& s1, F29& s2, const F29* __restrict__ rc29, uint32_t rf,
-                                             uint32_t rp) {
+                                             uint32_t rp, const uint4* __restrict__ qt) {
     if (COOP)
-        permute3_f29_coop<D>(s0, s1, s2, rc29, rf, rp);
+        permute3_f29_coop<D>(s0, s1, s2, rc29, rf, rp, qt);
     else
-        permute3_f29<D>(s0, s1, s2, rc29, rf, rp);
+        permute3_f29<D>(s0, s1, s2, rc29, rf, rp, qt);
 }
 
 // PaddingFreeSponge<Perm,3,2,1>::hash_iter over n elements read as ark-form Fr
 // by get(k); returns the ark-form (canonical) digest
 template <uint32_t D, bool COOP = false, class Get>
-__device__ __forceinline__ Fr sponge_f29(Get get, uint32_t n, const F29* rc29, uint32_t rf, uint32_t rp) {
+__device__ __forceinline__ Fr sponge_f29(Get get, uint32_t n, const F29* rc29, uint32_t rf, uint32_t rp,
+                                         const uint4* __restrict__ qt) {
     F29 s0 = f29_zero(), s1 = f29_zero(), s2 = f29_zero();
     // the next block is loaded before the current permutation, so its memory
     // latency hides behind ~46 K instructions instead of stalling the wave
@@ -184,20 +184,21 @@ __device__ __forceinline__ Fr sponge_f29(Get get, uint32_t n, const F29* rc29, u
         s1 = f29_from_fr(n1);
         if (k + 2 < n) n0 = get(k + 2);
         if (k + 3 < n) n1 = get(k + 3);
-        permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp);
+        permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp, qt);
         k += 2;
     }
     if (k < n) {
         s0 = f29_from_fr(n0);
-        permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp);
+        permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp, qt);
     }
     return f29_to_fr(s0);
 }
 
 template <uint32_t D, bool COOP = false>
-__device__ __forceinline__ Fr compress_f29(const Fr& l, const Fr& r, const F29* rc29, uint32_t rf, uint32_t rp) {
+__device__ __forceinline__ Fr compress_f29(const Fr& l, const Fr& r, const F29* rc29, uint32_t rf, uint32_t rp,
+                                           const uint4* __restrict__ qt) {
     F29 s0 = f29_from_fr(l), s1 = f29_from_fr(r), s2 = f29_zero();
-    permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp);
+    permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp, qt);
     return f29_to_fr(s0);
 }
 

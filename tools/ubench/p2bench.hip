@@ -29,21 +29,27 @@ __global__ void kconv_rc(const Fr* rc, F29* rc29, int n) {
     if (t < n) rc29[t] = f29_from_fr(rc[t]);
 }
 __global__ void kperm_check(Fr* st, Fr* st2, const Fr* rc, const F29* rc29, size_t n) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt table
+    f29_qtab_init(qt);
+    __syncthreads();
     size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= n) return;
     Fr a = st[3 * t], b = st[3 * t + 1], c = st[3 * t + 2];
     permute3<11>(a, b, c, rc, 8, 22);
     st[3 * t] = a; st[3 * t + 1] = b; st[3 * t + 2] = c;
     F29 x = f29_from_fr(st2[3 * t]), y = f29_from_fr(st2[3 * t + 1]), z = f29_from_fr(st2[3 * t + 2]);
-    permute3_f29<11>(x, y, z, rc29, 8, 22);
+    permute3_f29<11>(x, y, z, rc29, 8, 22, qt);
     st2[3 * t] = f29_to_fr(x); st2[3 * t + 1] = f29_to_fr(y); st2[3 * t + 2] = f29_to_fr(z);
 }
 template <int V> __global__ __launch_bounds__(256) void kperm_thr(Fr* out, const Fr* rc, const F29* rc29, int iters) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt table
+    f29_qtab_init(qt);
+    __syncthreads();
     size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     Fr a = fr_from_u64(t), b = fr_from_u64(t + 1), c = fr_zero();
     for (int i = 0; i < iters; ++i) {
         if (V == 0) { permute3<11>(a, b, c, rc, 8, 22); }
-        else { a = compress_f29<11>(a, b, rc29, 8, 22); }
+        else { a = compress_f29<11>(a, b, rc29, 8, 22, qt); }
     }
     out[t] = fr_add(fr_add(a, b), c);
 }
@@ -62,16 +68,22 @@ __global__ void kf29_lat(Fr* out, int iters) {
     out[threadIdx.x] = f29_to_fr(a);
 }
 template <int V> __global__ void kperm_lat(Fr* out, const Fr* rc, const F29* rc29, int iters) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt table
+    f29_qtab_init(qt);
+    __syncthreads();
     Fr a = fr_from_u64(threadIdx.x), b = fr_from_u64(threadIdx.x + 1), c = fr_zero();
     for (int i = 0; i < iters; ++i) {
-        if (V == 0) permute3<11>(a, b, c, rc, 8, 22); else a = compress_f29<11>(a, b, rc29, 8, 22);
+        if (V == 0) permute3<11>(a, b, c, rc, 8, 22); else a = compress_f29<11>(a, b, rc29, 8, 22, qt);
     }
     out[threadIdx.x] = fr_add(fr_add(a, b), c);
 }
 
 __global__ void kcoop_lat(Fr* out, const F29* rc29, int iters) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt table
+    f29_qtab_init(qt);
+    __syncthreads();
     Fr a = fr_from_u64(threadIdx.x >> 2), b = fr_from_u64((threadIdx.x >> 2) + 1);
-    for (int i = 0; i < iters; ++i) a = compress_f29<11, true>(a, b, rc29, 8, 22);
+    for (int i = 0; i < iters; ++i) a = compress_f29<11, true>(a, b, rc29, 8, 22, qt);
     out[threadIdx.x] = a;
 }
 

@@ -68,7 +68,11 @@ __device__ Fr fr_inv_f29(const Fr& a) {
 
 // n <= BI_BASE: per-thread chunks (stride BI_THREADS), a product tree over the
 // BI_THREADS chunk products in LDS, one inversion, back down the tree
-__global__ __launch_bounds__(BI_THREADS) void k_bi_base(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n) {
+// have_inv: the caller knows 1/(product of all n inputs) (inv_total), e.g. the
+// open phase's 1/(zeta^S - c^S) over a coset, and the Fermat inversion -- a
+// ~150 us chain of ~380 products on one lane -- is skipped
+__global__ __launch_bounds__(BI_THREADS) void k_bi_base(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n,
+                                                         Fr inv_total, int have_inv) {
     __shared__ Fr tree[2 * BI_THREADS];  // node k: children 2k, 2k+1; leaves at BI_THREADS + t
     const uint32_t t = threadIdx.x;
     Fr acc = fr_one();
@@ -82,7 +86,7 @@ __global__ __launch_bounds__(BI_THREADS) void k_bi_base(const Fr* __restrict__ i
         if (t < w) tree[w + t] = fr_mul(tree[2 * (w + t)], tree[2 * (w + t) + 1]);
         __syncthreads();
     }
-    if (t == 0) tree[1] = fr_inv_f29(tree[1]);
+    if (t == 0) tree[1] = have_inv ? inv_total : fr_inv_f29(tree[1]);
     __syncthreads();
     // top-down: node k holds 1/(product of its subtree); children swap products
     for (uint32_t w = 1; w < BI_THREADS; w <<= 1) {
@@ -178,7 +182,7 @@ size_t batch_inverse_scratch(size_t n) {
     return tot;
 }
 
-hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st, Fr* scratch) {
+hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st, Fr* scratch, const Fr* inv_total) {
     if (!n) return hipSuccess;
     if (!scratch && n > BI_BASE) {
         // lanes for one wave per SIMD (256 CUs x 4 SIMDs x 64), 8 .. 256 elements each
@@ -189,7 +193,8 @@ hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st,
         return hipGetLastError();
     }
     if (n <= BI_BASE) {
-        hipLaunchKernelGGL(k_bi_base, dim3(1), dim3(BI_THREADS), 0, st, in, out, n);
+        hipLaunchKernelGGL(k_bi_base, dim3(1), dim3(BI_THREADS), 0, st, in, out, n, inv_total ? *inv_total : fr_zero(),
+                           inv_total ? 1 : 0);
         return hipGetLastError();
     }
     const size_t T = (n + BI_CHUNK - 1) / BI_CHUNK;
@@ -198,7 +203,7 @@ hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st,
     hipLaunchKernelGGL(k_bi_up, dim3(nblocks(T, 256)), dim3(256), 0, st, in, out, n, T, BI_CHUNK, prod);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    e = launch_batch_inverse(prod, inv_prod, T, st, scratch + 2 * T);
+    e = launch_batch_inverse(prod, inv_prod, T, st, scratch + 2 * T, inv_total);  // same total product
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_bi_down, dim3(nblocks(T, 256)), dim3(256), 0, st, in, out, n, T, BI_CHUNK, inv_prod);
     return hipGetLastError();

@@ -79,7 +79,11 @@ hipError_t launch_merkle_levels(Fr* layers, size_t nleaves, size_t stop_len, con
 // elements (hierarchical, one Fermat inverse per call), or nullptr for the
 // single-level kernel (one inverse per 8..256 elements)
 size_t batch_inverse_scratch(size_t n);
-hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st, Fr* scratch = nullptr);
+// inv_total (optional, host value): 1/(product of all n inputs), when the caller
+// knows it in closed form -- the hierarchical path then skips its one Fermat
+// inversion (used only with a scratch buffer / n <= BI_BASE)
+hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st, Fr* scratch = nullptr,
+                                const Fr* inv_total = nullptr);
 // Fr-mul throughput probe: nthreads lanes x iters x 4 independent products
 hipError_t launch_calib_mul(Fr* out, size_t nthreads, uint32_t iters, hipStream_t st);
 // iters chained Poseidon2 permutations per lane, register-resident (k_hash.hip)

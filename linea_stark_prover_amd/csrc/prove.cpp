@@ -585,7 +585,14 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         Fr* inv_z = ctx->fbuf("o_invz", S);
         Fr* inv_zn = ctx->fbuf("o_invzn", S);
         LSP_HIP(launch_open_denoms(zeta, GEN, tabN, L1N, logN, S, dtmp, st, row0));
-        LSP_HIP(launch_batch_inverse(dtmp, inv_z, S, st, ctx->bi_scratch(S)));
+        // this rank's rows are the coset c H_S (c = GEN w_N^bitrev(row0)), so the
+        // product of its denominators is prod (zeta - c w) = zeta^S - c^S: its
+        // inverse on the host replaces the batch inverse's Fermat chain on the GPU
+        const Fr cS = fr_pow_u64(fr_mul(GEN, fr_pow_u64(host_two_adic_generator(logN), host_bitrev(row0, logN))), S);
+        const Fr den_prod = fr_sub(fr_pow_u64(zeta, S), cS);
+        LSP_REQUIRE(!fr_is_zero(den_prod), LSP_E_STATE, "zeta lies in the LDE domain");
+        const Fr den_prod_inv = fr_inv(den_prod);
+        LSP_HIP(launch_batch_inverse(dtmp, inv_z, S, st, ctx->bi_scratch(S), &den_prod_inv));
         LSP_HIP(launch_shift_inverse(inv_z, inv_zn, wh_inv, logN, 1ull << lb, row0, S, st));
         T.end("compute_inverse_denominators");
         T.begin("compute opened values with Lagrange interpolation");
@@ -904,10 +911,13 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         auto top_path = [&](const std::vector<std::vector<Fr>>& top, size_t sub, std::vector<Fr>& out) {
             for (uint32_t i = 0; i + 1 < top.size(); ++i) out.push_back(top[i][(sub >> i) ^ 1]);
         };
+        proof->queries.reserve(nq);
         for (uint32_t qi = 0; qi < nq; ++qi) {
             const size_t idx = idxs[qi], o = idx >> logS;
             const Fr* e = all.data() + (o * nq + qi) * E;
             lsp_query qq;
+            qq.sib.reserve(nr);
+            qq.fpath.reserve(nr);
             qq.trow.assign(e, e + w);
             e += w;
             qq.tpath.assign(e, e + logS);

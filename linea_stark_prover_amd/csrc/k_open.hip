@@ -2,6 +2,7 @@
 // 1/(z - GEN w_N^bitrev(i)), barycentric opened values (interpolate_coset),
 // the "reduce rows" accumulation, and the FRI fold
 // (TwoAdicFriGenericConfig::fold_matrix).
+#include "fr29.hpp"
 #include "k_common.hpp"
 #include "kernels.hpp"
 
@@ -77,20 +78,54 @@ __global__ __launch_bounds__(256) void k_sum_partials(const Fr* __restrict__ par
     if (threadIdx.x == 0) out[c] = red[0];
 }
 
+// One row of the FRI input: (ry_z - rr) / (z - x) + apw[w] (ry_zn - rr) / (zn - x)
+// + sum_j apw[2w+j] (ryq_j - qrow_j) / (z - x), rr = sum_k apw[k] row[k].
+// On the 29-bit-limb product (fr29.hpp): an ark-form element X = x 2^256 times
+// the 29-bit form W = w 2^261 gives X W 2^-261 = the ark form of x w, so the
+// constants (alpha powers) are converted once per workgroup into LDS and every
+// per-row factor (the inverse denominators) once per row; sums stay lazily
+// reduced (at most 3 products per limb-wise sum, then the LDS-table
+// reduction).  The result is canonical.
+constexpr uint32_t RR_CHUNK = 3;  // 3 normalised products + a value < 2r: limbs < 2^31, < 26.2 r (f29_reduce_qt)
 __global__ __launch_bounds__(256) void k_reduce_rows(ReduceArgs a) {
+    extern __shared__ uint4 rr_lds[];
+    uint4* qt = rr_lds;                                               // 3 * F29_QTAB_N
+    F29* apw29 = reinterpret_cast<F29*>(rr_lds + 3 * F29_QTAB_N);   // apw[0..w], apw[2w..2w+q): 29-bit form
+    F29* ryq_l = apw29 + a.w + 1 + a.q;                              // ryq[j] as limbs (ark form)
+    f29_qtab_init(qt);
+    for (uint32_t k = threadIdx.x; k < a.w + 1 + 2 * a.q; k += blockDim.x) {
+        if (k <= a.w)
+            apw29[k] = f29_from_fr(a.apw[k]);
+        else if (k < a.w + 1 + a.q)
+            apw29[k] = f29_from_fr(a.apw[2 * a.w + (k - a.w - 1)]);
+        else
+            ryq_l[k - a.w - 1 - a.q] = f29_repack_in(a.ryq[k - a.w - 1 - a.q]);
+    }
+    __syncthreads();
     const size_t i = gtid();
     if (i >= a.n) return;
     const Fr* row = a.lde + i * a.w;
-    Fr rr = fr_zero();
-    for (uint32_t k = 0; k < a.w; ++k) rr = fr_add(rr, fr_mul(a.apw[k], row[k]));
-    const Fr iz = a.inv_z[i];
-    Fr acc = fr_mul(fr_sub(a.ry_z, rr), iz);
-    acc = fr_add(acc, fr_mul(fr_mul(fr_sub(a.ry_zn, rr), a.inv_zn[i]), a.apw[a.w]));
+    F29 rr = f29_zero();
+    for (uint32_t k = 0; k < a.w; k += RR_CHUNK) {
+        F29 s = rr;
+        const uint32_t e = min(a.w, k + RR_CHUNK);
+        for (uint32_t c = k; c < e; ++c) s = f29_lazy2(s, f29_mul(f29_repack_in(row[c]), apw29[c]));  // < 8.06 r each
+        rr = f29_reduce_qt(s, qt);  // < 2 r
+    }
+    const F29 iz = f29_from_fr(a.inv_z[i]), izn = f29_from_fr(a.inv_zn[i]);  // 29-bit form, < 2 r
+    const F29 t1 = f29_mul(f29_sub16(f29_repack_in(a.ry_z), rr), iz);          // < 17 r in, < 8.1 r out
+    const F29 t2 = f29_mul(f29_mul(f29_sub16(f29_repack_in(a.ry_zn), rr), izn), apw29[a.w]);
     const Fr* qrow = a.qlde + i * a.q;
-    Fr qacc = fr_zero();
-    for (uint32_t j = 0; j < a.q; ++j) qacc = fr_add(qacc, fr_mul(a.apw[2 * a.w + j], fr_sub(a.ryq[j], qrow[j])));
-    acc = fr_add(acc, fr_mul(qacc, iz));
-    a.out[i] = acc;
+    F29 qacc = f29_zero();
+    for (uint32_t k = 0; k < a.q; k += RR_CHUNK) {
+        F29 s = qacc;
+        const uint32_t e = min(a.q, k + RR_CHUNK);
+        for (uint32_t j = k; j < e; ++j)
+            s = f29_lazy2(s, f29_mul(f29_sub16(ryq_l[j], f29_repack_in(qrow[j])), apw29[a.w + 1 + j]));
+        qacc = f29_reduce_qt(s, qt);
+    }
+    const F29 t3 = f29_mul(qacc, iz);
+    a.out[i] = fr_reduce_once(f29_repack_out(f29_reduce_qt(f29_lazy3(t1, t2, t3), qt)));  // < 24.3 r in
 }
 
 // coef[0..npts) = alpha offsets, coef[npts..2 npts) = offset * reduced ys; apw = alpha^c, c < w
@@ -146,7 +181,9 @@ hipError_t launch_sum_partials(const Fr* partial, uint32_t nb, uint32_t w, Fr* o
 }
 
 hipError_t launch_reduce_rows(const ReduceArgs& a, hipStream_t st) {
-    hipLaunchKernelGGL(k_reduce_rows, dim3(nblocks(a.n, 256)), dim3(256), 0, st, a);
+    const size_t lds = 3 * F29_QTAB_N * sizeof(uint4) + (a.w + 1 + 2 * (size_t)a.q) * sizeof(F29);
+    if (lds > 64 * 1024) return hipErrorInvalidValue;  // w + 2q up to ~1800 columns
+    hipLaunchKernelGGL(k_reduce_rows, dim3(nblocks(a.n, 256)), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 

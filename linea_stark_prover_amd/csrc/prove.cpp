@@ -205,19 +205,54 @@ static void host_compress_level(lsp_ctx* ctx, const Fr* in, Fr* out, size_t half
     }
 }
 
-// The levels above `first` digests host[0, first): each level compresses
-// pairs with the host pool and is appended; returns the end of the layers
-// (the root is host[end - 1]).  *t_first (if given) is set after the first level.
+// The levels above `first` digests host[0, first): each level is appended
+// after the one below it; returns the end of the layers (the root is
+// host[end - 1]).  *t_first (if given) is set after the first level.
+// Wide levels go level by level through the pool (work shared dynamically).
+// Once a level holds at most 16 digests per pool thread, the rest of the tree
+// is P = n / 16 subtrees of 16 digests, one task each (no barrier between their
+// levels: a parallel_for costs ~5 us, more than an 8-lane IFMA batch), and the
+// levels above the P subtree roots run on this thread.  The workers are awake
+// then (they just ran the level below).  LSP_HOST_SUBTREE=0: level by level.
 static size_t host_levels(lsp_ctx* ctx, Fr* host, size_t first,
                           std::chrono::steady_clock::time_point* t_first = nullptr) {
+    static const bool subtrees = [] {
+        const char* e = std::getenv("LSP_HOST_SUBTREE");
+        return !(e && *e == '0');
+    }();
+    constexpr size_t SUB = 16;  // digests per subtree task
+    HostPool& pool = ctx->host_pool();
     size_t lo = 0, n = first, end = first;
-    while (n > 1) {
+    while (n > 1 && (!subtrees || n > SUB * pool.size())) {
         host_compress_level(ctx, host + lo, host + end, n / 2);
         if (lo == 0 && t_first) *t_first = std::chrono::steady_clock::now();
         lo = end;
         end += n / 2;
         n /= 2;
     }
+    if (n <= 1) return end;
+    // n (a power of two, <= SUB * threads) digests at host[lo, lo + n): level
+    // j >= 1 above them holds n >> j digests at off[j]
+    size_t off[64];
+    uint32_t nl = 0;
+    off[0] = lo;
+    for (size_t c = n / 2; c >= 1; c /= 2) {
+        off[++nl] = end;
+        end += c;
+    }
+    auto level_part = [&](uint32_t j, size_t i0, size_t cnt) {  // level j, digests [i0, i0 + cnt)
+        if (cnt == 1)
+            host[off[j] + i0] = ctx->p2.compress(host[off[j - 1] + 2 * i0], host[off[j - 1] + 2 * i0 + 1]);
+        else
+            ctx->p2.compress_range(host + off[j - 1], host + off[j], i0, i0 + cnt);
+    };
+    const uint32_t sl = n >= SUB ? log2_exact(SUB) : 0;  // levels inside a subtree task
+    if (sl)
+        pool.parallel_for(n / SUB, [&](size_t p) {
+            for (uint32_t j = 1; j <= sl; ++j) level_part(j, p * (SUB >> j), SUB >> j);
+        });
+    for (uint32_t j = sl + 1; j <= nl; ++j) level_part(j, 0, n >> j);  // above the subtree roots
+    if (lo == 0 && t_first) *t_first = std::chrono::steady_clock::now();
     return end;
 }
 

@@ -331,6 +331,9 @@ int lsp_merkle_open(const lsp_tree* t, size_t index, lsp_fr* rows_out, lsp_fr* p
         LSP_REQUIRE(index < t->height, LSP_E_ARG, "index out of range");
         std::lock_guard<std::mutex> g(ctx->mu);
         need_gpu(ctx);
+        // the commit's host-made top layers go up asynchronously on the context's
+        // non-blocking stream; the copies below use the null stream
+        LSP_HIP(hipStreamSynchronize(ctx->stream));
         size_t o = 0;
         if (rows_out)
             for (size_t k = 0; k < t->mats.size(); ++k) {
@@ -362,7 +365,10 @@ int lsp_merkle_layer(const lsp_tree* t, uint32_t level, lsp_fr* out) {
         }
         std::lock_guard<std::mutex> g(ctx->mu);
         need_gpu(ctx);
-        LSP_HIP(hipMemcpy(out, t->layers + off, len * sizeof(Fr), hipMemcpyDeviceToHost));
+        // on the context's (non-blocking) stream: the host-made top layers are
+        // uploaded asynchronously on it by the commit
+        LSP_HIP(hipMemcpyAsync(out, t->layers + off, len * sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
+        LSP_HIP(hipStreamSynchronize(ctx->stream));
     });
 }
 

@@ -114,8 +114,11 @@ def test_hash_rows_matches_sponge(gpu_ctx, oracle_lib, w):
 
 
 # ---------------------------------------------------------------- Merkle
-@pytest.mark.parametrize("logh,widths", [(0, [3]), (1, [2]), (4, [8]), (10, [1, 1, 1, 1]), (12, [8]),
-                                         (13, [2]), (11, [3, 5])])
+# heights cover every host tree-top path (prove.cpp host_levels): below one
+# 16-digest subtree (2^3), one subtree (2^4), 16 subtree tasks (2^8), wide levels
+# first (2^9 .. 2^13), and trees hashed wholly on the host (h <= 1024, one matrix)
+@pytest.mark.parametrize("logh,widths", [(0, [3]), (1, [2]), (3, [2]), (4, [8]), (5, [1]), (8, [2]), (9, [3]),
+                                         (10, [1, 1, 1, 1]), (12, [8]), (13, [2]), (11, [3, 5])])
 def test_merkle_commit_open_verify(gpu_ctx, oracle_lib, logh, widths):
     from linea_stark_prover_amd.prover import MerkleTreeMmcs
     rng = np.random.default_rng(logh)
@@ -129,7 +132,10 @@ def test_merkle_commit_open_verify(gpu_ctx, oracle_lib, logh, widths):
     oracle_lib.lib().lo_merkle_commit(ctypes.byref(p), c_ptr(cat), ctypes.c_size_t(h), ctypes.c_size_t(cat.shape[1]),
                                       c_ptr(layers), 8)
     assert np.array_equal(root.reshape(4), layers[-1])
-    assert np.array_equal(tree.layer(0), layers[:h])
+    off = 0
+    for lv in range(logh + 1):  # every layer, GPU-made and host-made
+        assert np.array_equal(tree.layer(lv), layers[off:off + (h >> lv)]), f"layer {lv}"
+        off += h >> lv
     for idx in sorted({0, h - 1, h // 3}):
         rows, path = mmcs.open_batch(idx, tree)
         for m, r in zip(mats, rows):

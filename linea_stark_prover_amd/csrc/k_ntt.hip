@@ -50,6 +50,7 @@ struct NttPass {
     uint32_t nchunk;    // column chunks of 2^LOGCW per row
     uint32_t canon;     // 1: write canonical words (the transform's last pass)
     uint32_t xcd;       // 1: workgroup ids map to tiles XCD-aware (see k_ntt_rm)
+    uint32_t twl_n;     // PASS_INV_FWD: forward twiddles cached in LDS (G (2^k - 1) entries; 0: read from tw)
     uint64_t narr;      // arrays (cosets) in dst
 };
 
@@ -204,11 +205,27 @@ struct TileGeom {
     }
 };
 
+// The fused pass's forward twiddles, cached in LDS once per workgroup: its
+// tile rows are t 2^logL + gid (s0 = 0, logL + k = logH), so DIF stage s < k
+// reads w^(gid + (t mod 2^(k-1-s)) 2^logL) -- 2^(k-1-s) distinct values per row
+// group, G (2^k - 1) for the tile.  Read from the global table they were
+// fetched again for every coset (the tile's twiddles outgrow the L2 across the
+// workgroups of an XCD); from LDS, once.  Entry of (group g, stage s, u):
+// g (2^k - 1) + (2^k - 2^(k-s)) + u.
+template <int LOGCW>
+__device__ __forceinline__ uint32_t twl_index(const TileGeom<LOGCW>& gm, uint32_t row, uint32_t s) {
+    const uint32_t k = gm.k;
+    const uint32_t u = (row >> gm.logL) & ((1u << (k - 1 - s)) - 1);
+    const uint32_t g = (row & ((1u << gm.logL) - 1)) - gm.gid0;
+    return g * ((1u << k) - 1) + ((1u << k) - (1u << (k - s))) + u;
+}
+
 // stages s0 .. s0 + k - 1 of the tile in LDS: radix-4 groups of two stages,
 // then a radix-2 stage if k is odd; ends with a barrier
 template <bool DIF, int LOGCW>
 __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOGCW>& gm, const uint4* __restrict__ tw,
-                                            uint32_t s0, uint32_t logH, uint32_t n_el) {
+                                            uint32_t s0, uint32_t logH, uint32_t n_el,
+                                            const uint4* twl = nullptr) {
     constexpr uint32_t CW = 1u << LOGCW;
     const uint32_t k = gm.k, G = 1u << gm.logG;
     const uint32_t cshift = gm.logG + LOGCW;  // element index = (t << cshift) + (g << LOGCW) + c
@@ -218,6 +235,7 @@ __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOG
         // DIF w^((row mod H/2^(s+1)) 2^s), DIT w^((row mod 2^s) 2^(logH-1-s)); the
         // table is stage-major (entry 2^(m-1) - 1 + i = w_(2^m)^i), so
         // consecutive rows read consecutive slots
+        if (DIF && twl) return f29_load48(twl + 3 * twl_index(gm, row, s));  // the fused pass's LDS copy
         const uint32_t half = DIF ? (uint32_t)(H >> (s + 1)) : (1u << s);
         return f29_load48(tw + 3 * (size_t)(half - 1 + (row & (half - 1))));
     };
@@ -307,6 +325,27 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
     const TileLds T{lds_raw, lds_raw + n_el, reinterpret_cast<uint32_t*>(lds_raw + 2 * n_el)};
     constexpr uint32_t NREG = FWD_FIRST ? NTT_MAX_EL / NTT_THREADS : 1;
     F29 xr[NREG];
+    // the forward twiddles of this tile in LDS (after the tile and the per-row
+    // twist factors; published by the barrier after the coefficient load below)
+    uint4* twl = nullptr;
+    if (FWD_FIRST && p.twl_n) {
+        const bool rt = !p.twist_per_col;
+        twl = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_raw) + (size_t)n_el * sizeof(F29) +
+                                       (rt ? (size_t)(K << logG) * sizeof(F29) : 0));
+        const uint32_t per = K - 1;  // entries per row group
+        for (uint32_t e = threadIdx.x; e < p.twl_n; e += NTT_THREADS) {
+            const uint32_t g = e / per, r = e - g * per;
+            const uint32_t m = K - r;                       // 1 .. 2^k: stage s has m in (2^(k-1-s), 2^(k-s)]
+            const uint32_t s = p.k - (32 - __builtin_clz(m - 1 + (m == 1)));  // k - ceil(log2 m)
+            const uint32_t sk = m == 1 ? p.k - 1 : s;
+            const uint32_t u = r - (K - (K >> sk));
+            const uint32_t half = (uint32_t)(H >> (sk + 1));
+            const size_t gi = (size_t)(half - 1) + gm.gid0 + g + ((size_t)u << p.logL);
+            twl[3 * e] = p.tw[3 * gi];
+            twl[3 * e + 1] = p.tw[3 * gi + 1];
+            twl[3 * e + 2] = p.tw[3 * gi + 2];
+        }
+    }
     if (FWD_FIRST) {
         // ---- the inverse transform's last stages over these rows (logH - k ..
         // logH - 1; from the caller's rows, gathered bit-reversed, when the
@@ -376,7 +415,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
             }
         }
         __syncthreads();
-        tile_stages<DIF, LOGCW>(T, gm, p.tw, p.s0, p.logH, n_el);
+        tile_stages<DIF, LOGCW>(T, gm, p.tw, p.s0, p.logH, n_el, twl);
         // ---- store
         const bool canon = p.canon != 0;
         for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
@@ -466,6 +505,10 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
         const char* e = std::getenv("LSP_NTT_LOGCW");
         return e ? (uint32_t)std::min(3, std::max(0, std::atoi(e))) : 0u;
     }();
+    static const bool twl_env = [] {  // LSP_NTT_TWL=0: the fused pass reads its twiddles from HBM
+        const char* e = std::getenv("LSP_NTT_TWL");
+        return !(e && *e == '0');
+    }();
     static const uint32_t kmax_env = [] {
         const char* e = std::getenv("LSP_NTT_KMAX");
         return e ? (uint32_t)std::min(10, std::max(1, std::atoi(e))) : 10u;
@@ -509,7 +552,11 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
         const uint64_t tiles = (uint64_t)(mode == PASS_INV_FWD ? 1 : narr) * ((1ull << logh) >> (k + logG)) * nchunk;
         // tile, plus one twist factor per row in the fused pass
         const bool fac = mode == PASS_INV_FWD && !twist_per_col;
-        const size_t lds = ((size_t(1) << (k + logG)) * CW + (fac ? (size_t(1) << (k + logG)) : 0)) * sizeof(F29);
+        size_t lds = ((size_t(1) << (k + logG)) * CW + (fac ? (size_t(1) << (k + logG)) : 0)) * sizeof(F29);
+        // ... and its forward twiddles when they fit (<= 512 entries, 24 KiB: 2 workgroups per CU)
+        const size_t twl_n = (size_t(1) << logG) * ((size_t(1) << k) - 1);
+        p.twl_n = (mode == PASS_INV_FWD && twl_n <= 512 && twl_env) ? (uint32_t)twl_n : 0u;
+        lds += (size_t)p.twl_n * 3 * sizeof(uint4);
         p.xcd = (tiles / nchunk) % 8 == 0 ? 1u : 0u;
         const dim3 grid((unsigned)tiles), blk(256);
 #define LSP_NTT_LAUNCH(DIFV, MODEV)                                                                   \

@@ -105,6 +105,25 @@ inline F mul_u128(const F& a, const F& b) {
 }
 
 
+// x R^-1 (Montgomery form -> the integer), i.e. mul(x, 1) without the
+// products by b's limbs: four reduction rows of one imul + 4 multiplies.
+// Input < 2r (any value < 2^256 works: the result is < r + 1), output < 2r.
+inline F redc(const F& a) {
+    uint64_t t0 = a.l[0], t1 = a.l[1], t2 = a.l[2], t3 = a.l[3];
+    for (int i = 0; i < 4; ++i) {
+        const uint64_t m = t0 * NP;
+        u128 c = (u128)m * R0 + t0;
+        c = (u128)m * R1 + t1 + (uint64_t)(c >> 64);
+        t0 = (uint64_t)c;
+        c = (u128)m * R2 + t2 + (uint64_t)(c >> 64);
+        t1 = (uint64_t)c;
+        c = (u128)m * R3 + t3 + (uint64_t)(c >> 64);
+        t2 = (uint64_t)c;
+        t3 = (uint64_t)(c >> 64);
+    }
+    return F{{t0, t1, t2, t3}};
+}
+
 #if defined(__x86_64__) && defined(__ADX__) && defined(__BMI2__) && !defined(__HIP_DEVICE_COMPILE__)
 // The same CIOS (same digits m, same result bits) with mulx and the two carry
 // chains adcx / adox: ~30 % less latency than the compiler's code for

@@ -39,29 +39,29 @@ __global__ __launch_bounds__(256) void k_permute(Fr* __restrict__ st, size_t n, 
     st[3 * i + 2] = f29_to_fr(s2);
 }
 
-// COOP: one row per DPP quad (poseidon2_f29.hpp), for batches narrower than
-// the chip; otherwise one row per lane.
-template <uint32_t D, bool COOP>
+// LANES: lanes per row -- 4 (a DPP quad) or 2 (a pair) for batches narrower
+// than the chip (poseidon2_f29.hpp), otherwise 1.
+template <uint32_t D, int LANES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSP_P2_ROWS_WPE))) void k_hash_rows1(const Fr* __restrict__ m, uint32_t w, size_t nrows,
                                                     Fr* __restrict__ out, const F29* __restrict__ rc, uint32_t rf,
                                                     uint32_t rp) {
     __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
     f29_qtab_init(qt);
     __syncthreads();
-    const size_t i = COOP ? (gtid() >> 2) : gtid();
+    const size_t i = gtid() / LANES;
     if (i >= nrows) return;
     const Fr* row = m + i * w;
-    const Fr d = sponge_f29<D, COOP>([&](uint32_t k) { return row[k]; }, w, rc, rf, rp, qt);
-    if (!COOP || (threadIdx.x & 3) == 0) out[i] = d;
+    const Fr d = sponge_f29<D, LANES>([&](uint32_t k) { return row[k]; }, w, rc, rf, rp, qt);
+    if ((threadIdx.x & (LANES - 1)) == 0) out[i] = d;
 }
 
-template <uint32_t D, bool COOP>
+template <uint32_t D, int LANES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSP_P2_ROWS_WPE))) void k_hash_rows_multi(MatList ml, size_t nrows, Fr* __restrict__ out,
                                                          const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
     __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
     f29_qtab_init(qt);
     __syncthreads();
-    const size_t i = COOP ? (gtid() >> 2) : gtid();
+    const size_t i = gtid() / LANES;
     if (i >= nrows) return;
     uint32_t total = 0;
     for (uint32_t j = 0; j < ml.n; ++j) total += ml.width[j];
@@ -73,17 +73,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSP_P2_ROWS
         }
         return ml.ptr[j][i * ml.width[j] + k];
     };
-    const Fr d = sponge_f29<D, COOP>(get, total, rc, rf, rp, qt);
-    if (!COOP || (threadIdx.x & 3) == 0) out[i] = d;
+    const Fr d = sponge_f29<D, LANES>(get, total, rc, rf, rp, qt);
+    if ((threadIdx.x & (LANES - 1)) == 0) out[i] = d;
 }
 
-template <uint32_t D, bool COOP>
+template <uint32_t D, int LANES>
 __global__ __launch_bounds__(256) void k_fold_hash(FoldSpec f, size_t nleaves, Fr* __restrict__ out,
                                                    const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
     __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
     f29_qtab_init(qt);
     __syncthreads();
-    const size_t j = COOP ? (gtid() >> 2) : gtid();
+    const size_t j = gtid() / LANES;
     if (j >= nleaves) return;
     Fr e[2];
 #pragma unroll
@@ -92,24 +92,24 @@ __global__ __launch_bounds__(256) void k_fold_hash(FoldSpec f, size_t nleaves, F
         const Fr p = fr_mul(f.half_beta, pow2l(f.tab, f.L1, brev_bits(f.i0 + i, f.logm)));
         e[k] = fr_add(fr_mul(fr_add(f.half, p), f.v[2 * i]), fr_mul(fr_sub(f.half, p), f.v[2 * i + 1]));
     }
-    if (!COOP || (threadIdx.x & 3) == 0) {
+    if ((threadIdx.x & (LANES - 1)) == 0) {
         f.vout[2 * j] = e[0];
         f.vout[2 * j + 1] = e[1];
     }
-    const Fr d = sponge_f29<D, COOP>([&](uint32_t k) { return e[k]; }, 2, rc, rf, rp, qt);
-    if (!COOP || (threadIdx.x & 3) == 0) out[j] = d;
+    const Fr d = sponge_f29<D, LANES>([&](uint32_t k) { return e[k]; }, 2, rc, rf, rp, qt);
+    if ((threadIdx.x & (LANES - 1)) == 0) out[j] = d;
 }
 
-template <uint32_t D, bool COOP>
+template <uint32_t D, int LANES>
 __global__ __launch_bounds__(256) void k_merkle_level(const Fr* __restrict__ src, Fr* __restrict__ dst, size_t nout,
                                                       const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
     __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
     f29_qtab_init(qt);
     __syncthreads();
-    const size_t i = COOP ? (gtid() >> 2) : gtid();
+    const size_t i = gtid() / LANES;
     if (i >= nout) return;
-    const Fr d = compress_f29<D, COOP>(src[2 * i], src[2 * i + 1], rc, rf, rp, qt);
-    if (!COOP || (threadIdx.x & 3) == 0) dst[i] = d;
+    const Fr d = compress_f29<D, LANES>(src[2 * i], src[2 * i + 1], rc, rf, rp, qt);
+    if ((threadIdx.x & (LANES - 1)) == 0) dst[i] = d;
 }
 
 // Top of a tree in one workgroup of 4 * 64 lanes: `len` (<= 128, power of
@@ -130,7 +130,7 @@ __global__ __launch_bounds__(256) void k_merkle_top(Fr* __restrict__ layers, siz
     while (len > 1) {
         const uint32_t nout = len / 2;
         Fr r;
-        if (q < nout) r = compress_f29<D, true>(buf[2 * q], buf[2 * q + 1], rc, rf, rp, qt);
+        if (q < nout) r = compress_f29<D, 4>(buf[2 * q], buf[2 * q + 1], rc, rf, rp, qt);
         __syncthreads();
         if (q < nout && lead) {
             buf[q] = r;
@@ -200,22 +200,26 @@ hipError_t launch_rc_to_f29(const Fr* rc, F29* rc29, uint32_t n, hipStream_t st)
             hipLaunchKernelGGL(KERNEL<11>, __VA_ARGS__);                \
     } while (0)
 
-// (degree, coop) dispatch.  A batch of at most COOP_MAX permutations runs one
+// (degree, lanes) dispatch.  A batch of at most COOP_MAX permutations runs one
 // state per DPP quad: 4 * COOP_MAX lanes = one wave per SIMD of the 256 CUs,
 // where the quad form's shorter critical path (30 vs 46 S-boxes) wins; wider
 // batches are throughput-bound and keep one state per lane.
-#define LSP_DISPATCH_DC(L, COOP, KERNEL, ...)                             \
+#define LSP_DISPATCH_DC(L, LANES, KERNEL, ...)                            \
     do {                                                                  \
         if ((L).sbox_degree == 17) {                                      \
-            if (COOP)                                                     \
-                hipLaunchKernelGGL((KERNEL<17, true>), __VA_ARGS__);      \
+            if ((LANES) == 4)                                             \
+                hipLaunchKernelGGL((KERNEL<17, 4>), __VA_ARGS__);         \
+            else if ((LANES) == 2)                                        \
+                hipLaunchKernelGGL((KERNEL<17, 2>), __VA_ARGS__);         \
             else                                                          \
-                hipLaunchKernelGGL((KERNEL<17, false>), __VA_ARGS__);     \
+                hipLaunchKernelGGL((KERNEL<17, 1>), __VA_ARGS__);         \
         } else {                                                          \
-            if (COOP)                                                     \
-                hipLaunchKernelGGL((KERNEL<11, true>), __VA_ARGS__);      \
+            if ((LANES) == 4)                                             \
+                hipLaunchKernelGGL((KERNEL<11, 4>), __VA_ARGS__);         \
+            else if ((LANES) == 2)                                        \
+                hipLaunchKernelGGL((KERNEL<11, 2>), __VA_ARGS__);         \
             else                                                          \
-                hipLaunchKernelGGL((KERNEL<11, false>), __VA_ARGS__);     \
+                hipLaunchKernelGGL((KERNEL<11, 1>), __VA_ARGS__);         \
         }                                                                 \
     } while (0)
 
@@ -234,10 +238,21 @@ static unsigned coop_bs() {  // 0: by width (state_grid)
     return v;
 }
 #define COOP_MAX coop_max()
+// up to this many states a pair per state (2 lanes): at 32K states one wave per
+// SIMD with 168 instead of 230 products on each lane's critical path
+static size_t pair_max() {
+    static const size_t v = [] {
+        const char* e = std::getenv("LSP_PAIR_MAX");
+        return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)32768;
+    }();
+    return v;
+}
+static inline int lanes_for(size_t n) { return n <= COOP_MAX ? 4 : (n <= pair_max() ? 2 : 1); }
 
-// grid for n states: quads in 64-lane blocks when coop, else 256-lane blocks
-static inline void state_grid(size_t n, bool coop, unsigned& blocks, unsigned& bs) {
-    if (coop) {
+// grid for n states: quads in 64-lane blocks (256 from 16K states: one wave
+// per SIMD), pairs and single lanes in 256-lane blocks
+static inline void state_grid(size_t n, int lanes, unsigned& blocks, unsigned& bs) {
+    if (lanes == 4) {
         // 4 lanes per state.  At 16K states (one wave per SIMD of the chip) 64-lane
         // blocks land two waves on some SIMDs (~2x the level's latency); 256-lane
         // blocks, one per CU, spread them one per SIMD.  Narrower levels: 64.
@@ -245,7 +260,7 @@ static inline void state_grid(size_t n, bool coop, unsigned& blocks, unsigned& b
         blocks = nblocks(4 * n, bs);
     } else {
         bs = 256;
-        blocks = nblocks(n, bs);
+        blocks = nblocks((size_t)lanes * n, bs);
     }
 }
 
@@ -257,24 +272,24 @@ hipError_t launch_permute(Fr* states, size_t n, const F29* rc, P2Layout L, hipSt
 
 hipError_t launch_hash_rows(const MatList& m, size_t nrows, Fr* out, const F29* rc, P2Layout L, hipStream_t st) {
     if (!nrows) return hipSuccess;
-    const bool coop = nrows <= COOP_MAX;
+    const int lanes = lanes_for(nrows);
     unsigned blocks, bs;
-    state_grid(nrows, coop, blocks, bs);
+    state_grid(nrows, lanes, blocks, bs);
     if (m.n == 1)
-        LSP_DISPATCH_DC(L, coop, k_hash_rows1, dim3(blocks), dim3(bs), 0, st, m.ptr[0], m.width[0], nrows, out, rc,
+        LSP_DISPATCH_DC(L, lanes, k_hash_rows1, dim3(blocks), dim3(bs), 0, st, m.ptr[0], m.width[0], nrows, out, rc,
                         L.rounds_f, L.rounds_p);
     else
-        LSP_DISPATCH_DC(L, coop, k_hash_rows_multi, dim3(blocks), dim3(bs), 0, st, m, nrows, out, rc, L.rounds_f,
+        LSP_DISPATCH_DC(L, lanes, k_hash_rows_multi, dim3(blocks), dim3(bs), 0, st, m, nrows, out, rc, L.rounds_f,
                         L.rounds_p);
     return hipGetLastError();
 }
 
 hipError_t launch_fold_hash(const FoldSpec& f, size_t nleaves, Fr* out, const F29* rc, P2Layout L, hipStream_t st) {
     if (!nleaves) return hipSuccess;
-    const bool coop = nleaves <= COOP_MAX;
+    const int lanes = lanes_for(nleaves);
     unsigned blocks, bs;
-    state_grid(nleaves, coop, blocks, bs);
-    LSP_DISPATCH_DC(L, coop, k_fold_hash, dim3(blocks), dim3(bs), 0, st, f, nleaves, out, rc, L.rounds_f, L.rounds_p);
+    state_grid(nleaves, lanes, blocks, bs);
+    LSP_DISPATCH_DC(L, lanes, k_fold_hash, dim3(blocks), dim3(bs), 0, st, f, nleaves, out, rc, L.rounds_f, L.rounds_p);
     return hipGetLastError();
 }
 
@@ -294,10 +309,10 @@ hipError_t launch_grind(const Fr pre[3], uint32_t wlane, uint64_t base, uint64_t
 
 hipError_t launch_merkle_level(const Fr* src, Fr* dst, size_t nout, const F29* rc, P2Layout L, hipStream_t st) {
     if (!nout) return hipSuccess;
-    const bool coop = nout <= COOP_MAX;
+    const int lanes = lanes_for(nout);
     unsigned blocks, bs;
-    state_grid(nout, coop, blocks, bs);
-    LSP_DISPATCH_DC(L, coop, k_merkle_level, dim3(blocks), dim3(bs), 0, st, src, dst, nout, rc, L.rounds_f,
+    state_grid(nout, lanes, blocks, bs);
+    LSP_DISPATCH_DC(L, lanes, k_merkle_level, dim3(blocks), dim3(bs), 0, st, src, dst, nout, rc, L.rounds_f,
                     L.rounds_p);
     return hipGetLastError();
 }

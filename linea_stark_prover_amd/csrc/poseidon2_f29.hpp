@@ -87,6 +87,18 @@ __device__ __forceinline__ uint32_t quad_bcast(uint32_t x, int q) {
     }
 }
 
+// the same within lane pairs (0,1), (2,3) of a quad: quad_perm [0,0,2,2] / [1,1,3,3]
+__device__ __forceinline__ uint32_t pair_bcast(uint32_t x, int q) {
+    return q == 0 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xa0, 0xf, 0xf, false)
+                  : (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xf5, 0xf, 0xf, false);
+}
+
+// lane q (0 or 1) of this lane's group (a pair when LANES == 2, else a quad)
+template <int LANES>
+__device__ __forceinline__ uint32_t group_bcast(uint32_t x, int q) {
+    return LANES == 2 ? pair_bcast(x, q) : quad_bcast(x, q);
+}
+
 __device__ __forceinline__ F29 f29_sel3(uint32_t j, const F29& a, const F29& b, const F29& c) {
     // branch-free: masks instead of ?: (which the compiler turns into exec-mask branches)
     const uint32_t m0 = 0u - (uint32_t)(j == 0), m1 = 0u - (uint32_t)(j == 1), m2 = ~(m0 | m1);
@@ -114,7 +126,7 @@ __device__ __forceinline__ F29 full_round_coop(F29& s0, F29& s1, F29& s2, const 
 
 // partial-round S-box on a quad: x^11 = x^8 x^3 with x^4 (lane 0) and x^3
 // (lane 1) in parallel after x^2 -- four sequential products instead of five
-template <uint32_t D>
+template <uint32_t D, int LANES = 4>
 __device__ __forceinline__ F29 sbox29_coop(const F29& x) {
     if (D != 11) return sbox29<D>(x);
     const F29 x2 = f29_sqr(x);
@@ -122,14 +134,65 @@ __device__ __forceinline__ F29 sbox29_coop(const F29& x) {
     F29 sel;
 #pragma unroll
     for (int i = 0; i < 9; ++i) sel.l[i] = (x.l[i] & odd) | (x2.l[i] & ~odd);
-    const F29 y = f29_mul(x2, sel);  // lane 0: x^4, lane 1: x^3
+    const F29 y = f29_mul(x2, sel);  // even lane: x^4, odd lane: x^3
     F29 x4, x3;
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
-        x4.l[i] = quad_bcast(y.l[i], 0);
-        x3.l[i] = quad_bcast(y.l[i], 1);
+        x4.l[i] = group_bcast<LANES>(y.l[i], 0);
+        x3.l[i] = group_bcast<LANES>(y.l[i], 1);
     }
     return f29_mul(f29_sqr(x4), x3);
+}
+
+// ---- pair-cooperative permutation, for levels of 16K..32K states: a quad per
+// state would put two waves on a SIMD, one lane per state leaves half the SIMDs
+// idle.  The even lane of a pair computes S-box 0, the odd lane S-box 1, both
+// S-box 2; partial rounds as on a quad (x^4 and x^3 in parallel).  Critical
+// path: 2 rf + rp S-boxes' worth of products (8 x 10 + 22 x 4 = 168 against
+// 230 for one lane).  Both lanes of every pair must be active.
+template <uint32_t D>
+__device__ __forceinline__ F29 full_round_pair(F29& s0, F29& s1, F29& s2, const F29& t, const F29* __restrict__ c,
+                                               uint32_t odd) {
+    const uint32_t m1 = 0u - odd;
+    F29 in;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) in.l[i] = ((s0.l[i] + c[0].l[i]) & ~m1) | ((s1.l[i] + c[1].l[i]) & m1);
+    const F29 xa = sbox29<D>(f29_add(in, t));
+    s2 = sbox29<D>(f29_add(f29_lazy2(s2, c[2]), t));
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        s0.l[i] = pair_bcast(xa.l[i], 0);
+        s1.l[i] = pair_bcast(xa.l[i], 1);
+    }
+    return f29_lazy3(s0, s1, s2);
+}
+
+template <uint32_t D>
+__device__ __forceinline__ void permute3_f29_pair(F29& s0, F29& s1, F29& s2, const F29* __restrict__ rc29,
+                                                  uint32_t rf, uint32_t rp, const uint4* __restrict__ qt) {
+    const uint32_t odd = threadIdx.x & 1u;
+    const uint32_t half = rf / 2;
+    const F29* ini = rc29;
+    const F29* ter = rc29 + 3 * half;
+    const F29* itl = rc29 + 6 * half;
+    F29 t = f29_lazy3(s0, s1, s2);
+    for (uint32_t r = 0; r < half; ++r) t = full_round_pair<D>(s0, s1, s2, t, ini + 3 * r, odd);
+    F29 x = rp ? f29_add(f29_lazy2(s0, itl[0]), t) : f29_add(s0, t);
+    s1 = f29_reduce_qt(f29_lazy2(s1, t), qt);
+    s2 = f29_reduce_qt(f29_lazy2(s2, t), qt);
+    for (uint32_t r = 0; r < rp; ++r) {
+        const F29 y = sbox29_coop<D, 2>(x);
+        const F29 u = f29_reduce_qt(f29_lazy3(y, s1, s2), qt);
+        s1 = f29_reduce_qt(f29_lazy2(s1, u), qt);
+        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);
+        x = r + 1 < rp ? f29_add(f29_lazy2(y, itl[r + 1]), u) : f29_add(y, u);
+    }
+    s0 = x;
+    t = f29_zero();
+    for (uint32_t r = 0; r < half; ++r) t = full_round_pair<D>(s0, s1, s2, t, ter + 3 * r, odd);
+    s0 = f29_add(s0, t);
+    s1 = f29_add(s1, t);
+    s2 = f29_add(s2, t);
 }
 
 template <uint32_t D>
@@ -160,18 +223,21 @@ __device__ __forceinline__ void permute3_f29_coop(F29& s0, F29& s1, F29& s2, con
     s2 = f29_add(s2, t);
 }
 
-template <uint32_t D, bool COOP = false>
+// LANES: lanes per state (1, 2: pair_, 4: quad-cooperative)
+template <uint32_t D, int LANES = 1>
 __device__ __forceinline__ void permute3_any(F29& s0, F29& s1, F29& s2, const F29* __restrict__ rc29, uint32_t rf,
                                              uint32_t rp, const uint4* __restrict__ qt) {
-    if (COOP)
+    if (LANES == 4)
         permute3_f29_coop<D>(s0, s1, s2, rc29, rf, rp, qt);
+    else if (LANES == 2)
+        permute3_f29_pair<D>(s0, s1, s2, rc29, rf, rp, qt);
     else
         permute3_f29<D>(s0, s1, s2, rc29, rf, rp, qt);
 }
 
 // PaddingFreeSponge<Perm,3,2,1>::hash_iter over n elements read as ark-form Fr
 // by get(k); returns the ark-form (canonical) digest
-template <uint32_t D, bool COOP = false, class Get>
+template <uint32_t D, int LANES = 1, class Get>
 __device__ __forceinline__ Fr sponge_f29(Get get, uint32_t n, const F29* rc29, uint32_t rf, uint32_t rp,
                                          const uint4* __restrict__ qt) {
     F29 s0 = f29_zero(), s1 = f29_zero(), s2 = f29_zero();
@@ -184,21 +250,21 @@ __device__ __forceinline__ Fr sponge_f29(Get get, uint32_t n, const F29* rc29, u
         s1 = f29_from_fr(n1);
         if (k + 2 < n) n0 = get(k + 2);
         if (k + 3 < n) n1 = get(k + 3);
-        permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp, qt);
+        permute3_any<D, LANES>(s0, s1, s2, rc29, rf, rp, qt);
         k += 2;
     }
     if (k < n) {
         s0 = f29_from_fr(n0);
-        permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp, qt);
+        permute3_any<D, LANES>(s0, s1, s2, rc29, rf, rp, qt);
     }
     return f29_to_fr(s0);
 }
 
-template <uint32_t D, bool COOP = false>
+template <uint32_t D, int LANES = 1>
 __device__ __forceinline__ Fr compress_f29(const Fr& l, const Fr& r, const F29* rc29, uint32_t rf, uint32_t rp,
                                            const uint4* __restrict__ qt) {
     F29 s0 = f29_from_fr(l), s1 = f29_from_fr(r), s2 = f29_zero();
-    permute3_any<D, COOP>(s0, s1, s2, rc29, rf, rp, qt);
+    permute3_any<D, LANES>(s0, s1, s2, rc29, rf, rp, qt);
     return f29_to_fr(s0);
 }
 

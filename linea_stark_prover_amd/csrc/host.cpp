@@ -332,7 +332,7 @@ void lsp_ctx::release(const std::string& prefix) {
     }
 }
 
-void* lsp_ctx::hbuf(const std::string& name, size_t bytes) {
+void* lsp_ctx::hbuf(const std::string& name, size_t bytes, unsigned flags) {
     Buf& b = hpool[name];
     if (b.cap < bytes) {
         if (b.p) {
@@ -342,7 +342,7 @@ void* lsp_ctx::hbuf(const std::string& name, size_t bytes) {
             b.cap = 0;
         }
         if (bytes) {
-            if (hipHostMalloc(&b.p, bytes, hipHostMallocDefault) != hipSuccess) {
+            if (hipHostMalloc(&b.p, bytes, flags ? flags : hipHostMallocDefault) != hipSuccess) {
                 (void)hipGetLastError();
                 throw lsp::LspError(LSP_E_OOM, "hipHostMalloc(" + std::to_string(bytes) + ") for " + name + " failed");
             }

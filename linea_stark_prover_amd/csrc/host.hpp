@@ -296,7 +296,9 @@ struct lsp_ctx {
     // scratch of a hierarchical batch inverse of n elements (launch_batch_inverse)
     lsp::Fr* bi_scratch(size_t n) { return fbuf("bi_scratch", lsp::batch_inverse_scratch(n) + 1); }
     // pinned host memory; growing it first drains the stream (a copy may still read it)
-    void* hbuf(const std::string& name, size_t bytes);
+    // pinned host staging buffer `name`, grown on demand; flags: hipHostMalloc
+    // flags (hipHostMallocCoherent for buffers kernels write into directly)
+    void* hbuf(const std::string& name, size_t bytes, unsigned flags = 0);
     // asynchronous upload of a small host array through the pinned staging
     // buffer `name`: the caller's memory may be reused at return and the
     // stream is not drained (only the previous copy out of `name` is awaited)

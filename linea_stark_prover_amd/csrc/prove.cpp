@@ -282,6 +282,15 @@ struct DeferTopUploads {
     }
 };
 
+// LSP_TOP_ZEROCOPY=0: the last GPU level goes to HBM and a copy brings it to the host
+static bool zerocopy_top() {
+    static const bool on = [] {
+        const char* e = std::getenv("LSP_TOP_ZEROCOPY");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
 Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, const FoldSpec* fold) {
     hipStream_t st = ctx->stream;
     using clk = std::chrono::steady_clock;
@@ -298,6 +307,7 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
         fold = nullptr;
     }
     const bool leaves_on_host = height <= top && m.n == 1 && height > 1;
+    bool gpu_level_on_host = false;  // the last GPU level was written into `host` directly
     Fr* host;  // host layers, starting at device offset `off` (pinned)
     if (leaves_on_host) {
         const size_t w = m.width[0];
@@ -325,10 +335,32 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
             LSP_HIP(hipEventCreateWithFlags(&ctx->ev_top, hipEventDisableTiming));
         }
         LSP_HIP(hipEventRecord(ctx->ev_near, st));
-        LSP_HIP(launch_merkle_levels(layers + off1, len1, top, ctx->rc29_dev, ctx->p2.L, &off, &len, st));
-        off += off1;
-        host = (Fr*)ctx->hbuf(top_buf_name(ctx), (2 * len - 1) * sizeof(Fr));
-        LSP_HIP(hipMemcpyAsync(host, layers + off, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
+        size_t off2 = 0, len2 = len1;
+        if (zerocopy_top())
+            LSP_HIP(launch_merkle_levels(layers + off1, len1, 2 * top, ctx->rc29_dev, ctx->p2.L, &off2, &len2, st));
+        if (zerocopy_top() && len2 > top) {
+            // down to 2 top digests in HBM; the last GPU level writes its `top`
+            // digests straight into the pinned host buffer (no copy kernel on the
+            // critical path); the upload below takes them back to HBM
+            off = off1 + off2;
+            len = len2 / 2;
+            // fine-grained (coherent) pinned memory: the kernel's stores bypass the
+            // GPU caches, so they are in host memory when the kernel completes
+            host = (Fr*)ctx->hbuf(top_buf_name(ctx) + "c", (2 * len - 1) * sizeof(Fr), hipHostMallocCoherent);
+            LSP_HIP(launch_merkle_level(layers + off, host, len, ctx->rc29_dev, ctx->p2.L, st));
+            off += len2;
+            gpu_level_on_host = true;
+        } else if (zerocopy_top()) {  // no GPU level left above `top` digests: copy them
+            off = off1 + off2;
+            len = len2;
+            host = (Fr*)ctx->hbuf(top_buf_name(ctx), (2 * len - 1) * sizeof(Fr));
+            LSP_HIP(hipMemcpyAsync(host, layers + off, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
+        } else {
+            LSP_HIP(launch_merkle_levels(layers + off1, len1, top, ctx->rc29_dev, ctx->p2.L, &off, &len, st));
+            off += off1;
+            host = (Fr*)ctx->hbuf(top_buf_name(ctx), (2 * len - 1) * sizeof(Fr));
+            LSP_HIP(hipMemcpyAsync(host, layers + off, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
+        }
         LSP_HIP(hipEventRecord(ctx->ev_top, st));
         // sleep through the wide levels, then spin (with the pool awake) for the last ones
         LSP_HIP(hipEventSynchronize(ctx->ev_near));
@@ -352,7 +384,8 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
         g_top_times.levels_us += std::chrono::duration<double, std::micro>(tt3 - tt1).count();
         g_top_times.first_us += std::chrono::duration<double, std::micro>(tt2 - tt1).count();
     }
-    const size_t skip = leaves_on_host ? 0 : first;  // host-made digests start here
+    // digests that exist only on the host start here
+    const size_t skip = leaves_on_host || gpu_level_on_host ? 0 : first;
     if (end > skip) {
         if (ctx->defer_top_uploads)
             ctx->top_uploads.push_back({layers + off + skip, host + skip, (end - skip) * sizeof(Fr)});

@@ -193,6 +193,10 @@ int lsp_ctx_destroy(lsp_ctx* ctx) {
     for (auto& kv : ctx->twiddles) (void)hipFree(kv.second);
     for (auto& kv : ctx->stage_ev) (void)hipEventDestroy(kv.second);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+    for (auto& t : ctx->pending_timings) {
+        (void)hipEventDestroy(std::get<1>(t));
+        (void)hipEventDestroy(std::get<2>(t));
+    }
     if (ctx->ev_near) (void)hipEventDestroy(ctx->ev_near);
     if (ctx->ev_top) (void)hipEventDestroy(ctx->ev_top);
     if (ctx->rc_dev) (void)hipFree(ctx->rc_dev);
@@ -878,6 +882,11 @@ int lsp_verify(const lsp_ctx* ctx, const int32_t* air, size_t air_len, const lsp
 
 int lsp_last_timings(const lsp_ctx* ctx, double* ms, const char** names, size_t cap, size_t* n) {
     if (!ctx || !n) return LSP_E_ARG;
+    try {
+        lsp::resolve_timings(const_cast<lsp_ctx*>(ctx));  // the events are the context's own
+    } catch (...) {
+        return LSP_E_HIP;
+    }
     *n = ctx->timings.size();
     for (size_t i = 0; i < ctx->timings.size() && i < cap; ++i) {
         if (ms) ms[i] = ctx->timings[i].second;

@@ -11,6 +11,7 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <tuple>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -285,6 +286,10 @@ struct lsp_ctx {
     std::map<uint32_t, std::vector<lsp::Fr>> fold_tw;  // host FRI fold factors g^-bitrev(i) per log2 length (prove.cpp)
     size_t fri_host_tail = 2048;  // FRI rounds of at most this many leaves run wholly on the host (prove.cpp)
     std::vector<std::pair<std::string, double>> timings;
+    // the last proof's phase events, turned into `timings` lazily
+    // (resolve_timings): while the next proof sleeps through its first wide
+    // Merkle levels, or when lsp_last_timings asks -- not on the proof's tail
+    std::vector<std::tuple<std::string, hipEvent_t, hipEvent_t>> pending_timings;
     // the last proof's data-shaped spans in the reference's bench.log wording
     // (prove.cpp; lsp_last_spans)
     std::vector<std::string> spans;

@@ -190,6 +190,13 @@ LSP_IFMA W add(const W& a, const V& c) { return W{add(a.x, c), add(a.y, c)}; }
 template <uint32_t D, class T>
 LSP_IFMA T sbox_t(const T& x) {
     const T x2 = mul(x, x);
+#ifndef LSP_HOST_SBOX5  // x^3 and x^4 side by side: 4 dependent products (poseidon2_host64.hpp)
+    if (D == 11) {
+        const T x3 = mul(x2, x);
+        const T x4 = mul(x2, x2);
+        return mul(mul(x4, x4), x3);
+    }
+#endif
     const T x4 = mul(x2, x2);
     const T x8 = mul(x4, x4);
     if (D == 11) return mul(mul(x8, x2), x);

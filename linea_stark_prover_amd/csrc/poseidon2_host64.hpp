@@ -76,6 +76,19 @@ inline F add(const F& a, const F& b) {
     return csub(s, D0, D1, D2, D3);
 }
 
+// a - b as a + (2r - b), for b < 2r: < 4r, then one conditional subtraction of 2r
+inline F sub(const F& a, const F& b) {
+    F n;
+    u128 c = (u128)D0 - b.l[0];
+    n.l[0] = (uint64_t)c;
+    c = (u128)D1 - b.l[1] - (uint64_t)((c >> 64) & 1);
+    n.l[1] = (uint64_t)c;
+    c = (u128)D2 - b.l[2] - (uint64_t)((c >> 64) & 1);
+    n.l[2] = (uint64_t)c;
+    n.l[3] = D3 - b.l[3] - (uint64_t)((c >> 64) & 1);
+    return add(a, n);
+}
+
 inline F mul_u128(const F& a, const F& b) {
     uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
     for (int i = 0; i < 4; ++i) {
@@ -215,9 +228,19 @@ inline F mul(const F& a, const F& b) {
 inline F mul(const F& a, const F& b) { return mul_u128(a, b); }
 #endif
 
+// x^11 = (x^4)^2 x^3 with x^3 and x^4 independent: a chain of 4 products
+// instead of 5 (the core runs the two middle ones side by side) -- the host's
+// permutations are latency-bound (tree tops, transcript samples)
 template <uint32_t D>
 inline F sbox(const F& x) {
     const F x2 = mul(x, x);
+#ifndef LSP_HOST_SBOX5  // A/B switch: the 5-product chain x^8 x^2 x
+    if (D == 11) {
+        const F x3 = mul(x2, x);
+        const F x4 = mul(x2, x2);
+        return mul(mul(x4, x4), x3);
+    }
+#endif
     const F x4 = mul(x2, x2);
     const F x8 = mul(x4, x4);
     if (D == 11) return mul(mul(x8, x2), x);

@@ -53,22 +53,35 @@ struct PhaseTimer {
             }
         }
     }
+    // hand the phase events over for resolve_timings (no wait here: ~40 us of
+    // event queries at the end of every proof otherwise)
     void collect() {
+        resolve_timings(ctx);  // a previous proof's, if nobody asked for them
         ctx->timings.clear();
-        LSP_HIP(hipStreamSynchronize(ctx->stream));
-        for (auto& t : done) {
-            float ms = 0;
-            LSP_HIP(hipEventElapsedTime(&ms, std::get<1>(t), std::get<2>(t)));
-            ctx->timings.emplace_back(std::get<0>(t), (double)ms);
-            ctx->event_pool.push_back(std::get<1>(t));
-            ctx->event_pool.push_back(std::get<2>(t));
-        }
+        ctx->pending_timings = std::move(done);
         for (auto& st : starts) ctx->event_pool.push_back(st.second);
         done.clear();
         starts.clear();
     }
 };
 
+}  // namespace
+
+void resolve_timings(lsp_ctx* ctx) {
+    if (ctx->pending_timings.empty()) return;
+    ctx->timings.clear();
+    for (auto& t : ctx->pending_timings) {
+        LSP_HIP(hipEventSynchronize(std::get<2>(t)));
+        float ms = 0;
+        LSP_HIP(hipEventElapsedTime(&ms, std::get<1>(t), std::get<2>(t)));
+        ctx->timings.emplace_back(std::get<0>(t), (double)ms);
+        ctx->event_pool.push_back(std::get<1>(t));
+        ctx->event_pool.push_back(std::get<2>(t));
+    }
+    ctx->pending_timings.clear();
+}
+
+namespace {
 void two_level(uint32_t bits, uint32_t& L1, uint32_t& L2) {
     L1 = (bits + 1) / 2;
     L2 = bits - L1;
@@ -172,10 +185,20 @@ struct TopTimes {
     bool on = std::getenv("LSP_TIME_TOPS") != nullptr;
     double sync_us = 0, levels_us = 0, first_us = 0;
     size_t n = 0;
+    // per tree (the last ones are printed): host time since the previous tree's
+    // return, launch issue, sleep until ev_near, spin until ev_top, host levels
+    struct Rec { size_t height; double since_prev, launch, near, spin, levels; };
+    std::vector<Rec> recs;
+    std::chrono::steady_clock::time_point last_exit{};
     ~TopTimes() {
-        if (on && n)
+        if (on && n) {
             std::fprintf(stderr, "[tree tops] %zu trees: wait-for-GPU %.1f us, host levels %.1f us (first level %.1f us) per tree\n",
                          n, sync_us / n, levels_us / n, first_us / n);
+            const size_t k = recs.size() < 16 ? 0 : recs.size() - 16;
+            for (size_t i = k; i < recs.size(); ++i)
+                std::fprintf(stderr, "[tree] height %9zu  since-prev %7.1f  launch %6.1f  near %8.1f  spin %7.1f  levels %6.1f us\n",
+                             recs[i].height, recs[i].since_prev, recs[i].launch, recs[i].near, recs[i].spin, recs[i].levels);
+        }
     }
 };
 static TopTimes g_top_times;
@@ -295,6 +318,7 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
     hipStream_t st = ctx->stream;
     using clk = std::chrono::steady_clock;
     const auto tt0 = clk::now();
+    auto t_launched = tt0, t_near = tt0;
     size_t top = ctx->host_tree_top;
     if (g_active_proofs.load(std::memory_order_relaxed) > 1) top = std::min(top, SHARED_HOST_TREE_TOP);
     if (const char* e = std::getenv("LSP_HOST_TREE_TOP")) top = std::strtoull(e, nullptr, 10);
@@ -362,8 +386,11 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
             LSP_HIP(hipMemcpyAsync(host, layers + off, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
         }
         LSP_HIP(hipEventRecord(ctx->ev_top, st));
+        t_launched = clk::now();
         // sleep through the wide levels, then spin (with the pool awake) for the last ones
+        resolve_timings(ctx);  // the previous proof's phase events, meanwhile
         LSP_HIP(hipEventSynchronize(ctx->ev_near));
+        t_near = clk::now();
         pool.wake();
         hipError_t q;
         while ((q = hipEventQuery(ctx->ev_top)) == hipErrorNotReady) {
@@ -383,6 +410,10 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
         g_top_times.sync_us += std::chrono::duration<double, std::micro>(tt1 - tt0).count();
         g_top_times.levels_us += std::chrono::duration<double, std::micro>(tt3 - tt1).count();
         g_top_times.first_us += std::chrono::duration<double, std::micro>(tt2 - tt1).count();
+        auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        g_top_times.recs.push_back({height, g_top_times.last_exit == clk::time_point{} ? 0.0 : us(g_top_times.last_exit, tt0),
+                                    us(tt0, t_launched), us(t_launched, t_near), us(t_near, tt1), us(tt1, tt3)});
+        g_top_times.last_exit = clk::now();
     }
     // digests that exist only on the host start here
     const size_t skip = leaves_on_host || gpu_level_on_host ? 0 : first;
@@ -799,14 +830,17 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                 const size_t rounds_gpu = rounds.size();
                 HostPool& pool = ctx->host_pool();
                 size_t hvo = 0, hto = 0;
+                const size_t to0 = to, vo0 = vo, len0 = len;
                 while (len > final_len) {
                     const size_t m = len / 2;
                     const uint32_t logm = log2_exact(m);
                     const Fr* v = hv + hvo;
                     Fr* lay = htr + hto;
+                    const auto tr0 = std::chrono::steady_clock::now();
                     host_compress_level(ctx, v, lay, m);  // a 2-element leaf's hash_iter is compress (A4/A5)
+                    const auto tr1 = std::chrono::steady_clock::now();
                     const size_t end = host_levels(ctx, lay, m);
-                    LSP_HIP(hipMemcpyAsync(ftree + to, lay, end * sizeof(Fr), hipMemcpyHostToDevice, st));
+                    const auto tr2 = std::chrono::steady_clock::now();
                     FriRound R;
                     R.vec = fv + vo;
                     R.tree = ftree + to;
@@ -826,13 +860,29 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                         for (size_t i = 0; i < m; ++i) tw[i] = pw[host_bitrev(i, logm)];
                     }
                     Fr* out = hv + hvo + len;
-                    pool.parallel_for((m + 63) / 64, [&](size_t blk) {
-                        for (size_t i = 64 * blk; i < std::min(m, 64 * blk + 64); ++i) {
-                            const Fr p = fr_mul(hb, tw[i]);
-                            out[i] = fr_add(fr_mul(fr_add(half, p), v[2 * i]), fr_mul(fr_sub(half, p), v[2 * i + 1]));
+                    // half (v0 + v1) + hb g^-bitrev(i) (v0 - v1), in the 64-bit lazy
+                    // form; short vectors on this thread (a pool round trip costs more)
+                    const hp64::F hh = hp64::from(half), hbb = hp64::from(hb);
+                    auto fold_blk = [&](size_t i0, size_t i1) {
+                        for (size_t i = i0; i < i1; ++i) {
+                            const hp64::F a = hp64::from(v[2 * i]), b = hp64::from(v[2 * i + 1]);
+                            const hp64::F p = hp64::mul(hbb, hp64::from(tw[i]));
+                            out[i] = hp64::to_canonical(hp64::add(hp64::mul(hh, hp64::add(a, b)),
+                                                                  hp64::mul(p, hp64::sub(a, b))));
                         }
-                    });
-                    LSP_HIP(hipMemcpyAsync(fv + vo + len, out, m * sizeof(Fr), hipMemcpyHostToDevice, st));
+                    };
+                    if (m <= 256)
+                        fold_blk(0, m);
+                    else
+                        pool.parallel_for((m + 63) / 64, [&](size_t blk) { fold_blk(64 * blk, std::min(m, 64 * blk + 64)); });
+                    if (g_top_times.on) {
+                        const auto tr3 = std::chrono::steady_clock::now();
+                        auto us = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+                            return std::chrono::duration<double, std::micro>(b - a).count();
+                        };
+                        std::fprintf(stderr, "[fri tail round] m %5zu  leaves %6.1f  levels %6.1f  challenge+fold+copies %6.1f us\n",
+                                     m, us(tr0, tr1), us(tr1, tr2), us(tr2, tr3));
+                    }
                     rounds.push_back(std::move(R));
                     hvo += len;
                     vo += len;
@@ -841,6 +891,10 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                     len = m;
                 }
                 hfin = hv + hvo;
+                // every round's layers and folded vector back to the device (for the
+                // query gather): both are contiguous, so two copies instead of two per round
+                LSP_HIP(hipMemcpyAsync(ftree + to0, htr, (to - to0) * sizeof(Fr), hipMemcpyHostToDevice, st));
+                LSP_HIP(hipMemcpyAsync(fv + vo0 + len0, hv + len0, (hvo + len - len0) * sizeof(Fr), hipMemcpyHostToDevice, st));
                 if (g_top_times.on)
                     std::fprintf(stderr, "[fri tail] %zu rounds on the host: %.1f us (download %.1f us)\n",
                                  rounds.size() - rounds_gpu,

@@ -11,6 +11,8 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
 // leaves + every layer into `layers` (2*height - 1); returns the root
 // fold: when set, the leaves are the pairs of the FRI fold it describes (fused
 // into the leaf kernel; m.ptr[0] receives the folded vector)
+// the pending phase events of the last proof -> ctx->timings (prove.cpp)
+void resolve_timings(lsp_ctx* ctx);
 Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, const FoldSpec* fold = nullptr);
 lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, const Air& air, const Fr* pub,
                         size_t npub);

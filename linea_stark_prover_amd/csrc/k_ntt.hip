@@ -72,8 +72,13 @@ __device__ __forceinline__ F29 f29_load48(const uint4* __restrict__ q) {
     return o;
 }
 
+// A tile value to ark words.  Between passes the arrays keep the values as the
+// stages leave them (normalised, < 8.3 r < 2^256: the invariant inside a pass,
+// which the next pass's loads accept); the transform's last stage is trivial
+// and reduces its outputs below 2r, so the last pass (canon) needs only one
+// conditional subtraction.  No product-sized reduction on any store.
 __device__ __forceinline__ Fr f29_store(const F29& v, bool canon) {
-    const Fr o = f29_repack_out(f29_reduce(v));  // < 2r
+    const Fr o = f29_repack_out(v);
     return canon ? fr_reduce_once(o) : o;
 }
 
@@ -134,9 +139,13 @@ struct TileLds {
 // DIF stages s (distance D) and s + 1 (D/2) on v0..v3 = positions t0, t0 + D/2,
 // t0 + D, t0 + 3D/2: wA = w(s, t0), wA2 = w(s, t0 + D/2), wB = w(s + 1, t0)
 // (= w(s + 1, t0 + D)); trivB: stage s + 1 is the transform's last (w = 1).
+// u0 stays carry-free (limbs < 2^30): as the minuend of f29_sub32 it makes
+// limbs < 2^31 and column sums < 2^63.74 in the product by wB
+// (tools/gen_fr29mul.py --bound), and f29_reduce takes it as it is (its
+// quotient estimate from the top limb still leaves < 2r).
 __device__ __forceinline__ void dif4(F29& v0, F29& v1, F29& v2, F29& v3, const F29& wA, const F29& wA2,
                                      const F29& wB, bool trivB) {
-    const F29 u0 = f29_norm(f29_lazy2(v0, v2));       // < 16.6 r
+    const F29 u0 = f29_lazy2(v0, v2);                  // < 16.6 r, limbs < 2^30
     const F29 u2 = f29_mul(f29_sub16(v0, v2), wA);    // < 8.06 r
     const F29 u1 = f29_norm(f29_lazy2(v1, v3));
     const F29 u3 = f29_mul(f29_sub16(v1, v3), wA2);

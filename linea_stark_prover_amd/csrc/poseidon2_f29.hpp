@@ -9,10 +9,13 @@
 //     folded into the next S-box input with the round constant: inputs
 //     < 4 Y + 2 inside a permutation (Y = the S-box output bound), < 8 Y + 6
 //     at the start of a sponge permutation (s2 carries over);
-//   partial rounds: u = reduce(y + s1 + s2) < 2 r, s1 = reduce(s1 + u),
-//     s2 = reduce(2 s2 + u): limb-wise sums (< 13.7 r, limbs < 1.5 2^30)
-//     into the LDS-table reduction f29_reduce_qt (`qt`, valid below 64 r),
-//     so s1 and s2 stay < 2 r for any number of partial rounds;
+//   partial rounds: u = reduce(y + s1 + s2) < 2 r, s2 = reduce(2 s2 + u),
+//     s1 = s1 + u carry-free in even rounds (limbs < 2^30, < 4 r) and
+//     reduce(s1 + u) in odd ones: limb-wise sums (< 15.7 r, limbs < 2^31)
+//     into the LDS-table reduction f29_reduce_qt (`qt`, valid below 64 r
+//     with limbs < 2.41 2^30), so s2 stays < 2 r and s1 < 4 r for any number
+//     of partial rounds (a lazy s1 enters the terminal full rounds through a
+//     carry-propagating add);
 //   the output state is normalised and < 4 Y.
 #pragma once
 #include "fr29.hpp"
@@ -27,6 +30,14 @@ __device__ __forceinline__ F29 sbox29(const F29& x) {
     if (D == 11) return f29_mul(f29_mul(x8, x2), x);
     return f29_mul(f29_sqr(x8), x);  // x^17
 }
+
+
+// The partial rounds two at a time (no branch inside the pair): s1 carry-free
+// after the first, reduced after the second (header); an odd last round
+// reduces it.  LANES: 1 (one state per lane) or 2 / 4 (cooperative S-box).
+template <uint32_t D, int LANES>
+__device__ __forceinline__ F29 partial_rounds_f29(F29 x, F29& s1, F29& s2, const F29* __restrict__ itl, uint32_t rp,
+                                                  const uint4* __restrict__ qt);
 
 // rc29: round constants in F29 form, new_from_rng order (initial external
 // [rf/2][3], terminal external [rf/2][3], internal [rp])
@@ -49,13 +60,7 @@ __device__ __forceinline__ void permute3_f29(F29& s0, F29& s1, F29& s2, const F2
     F29 x = rp ? f29_add(f29_lazy2(s0, itl[0]), t) : f29_add(s0, t);
     s1 = f29_reduce_qt(f29_lazy2(s1, t), qt);  // < 38.8 r, limbs < 2^31
     s2 = f29_reduce_qt(f29_lazy2(s2, t), qt);
-    for (uint32_t r = 0; r < rp; ++r) {
-        const F29 y = sbox29<D>(x);
-        const F29 u = f29_reduce_qt(f29_lazy3(y, s1, s2), qt);  // < 13.7 r
-        s1 = f29_reduce_qt(f29_lazy2(s1, u), qt);
-        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);
-        x = r + 1 < rp ? f29_add(f29_lazy2(y, itl[r + 1]), u) : f29_add(y, u);
-    }
+    x = partial_rounds_f29<D, 1>(x, s1, s2, itl, rp, qt);
     s0 = x;
     t = f29_zero();
     for (uint32_t r = 0; r < half; ++r) {
@@ -144,6 +149,39 @@ __device__ __forceinline__ F29 sbox29_coop(const F29& x) {
     return f29_mul(f29_sqr(x4), x3);
 }
 
+
+template <uint32_t D, int LANES>
+__device__ __forceinline__ F29 partial_rounds_f29(F29 x, F29& s1, F29& s2, const F29* __restrict__ itl, uint32_t rp,
+                                                  const uint4* __restrict__ qt) {
+    auto sb = [](const F29& v) {
+        if constexpr (LANES == 1)
+            return sbox29<D>(v);
+        else
+            return sbox29_coop<D, LANES>(v);
+    };
+    uint32_t r = 0;
+    for (; r + 2 <= rp; r += 2) {
+        F29 y = sb(x);
+        F29 u = f29_reduce_qt(f29_lazy3(y, s1, s2), qt);
+        s1 = f29_lazy2(s1, u);
+        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);
+        x = f29_add(f29_lazy2(y, itl[r + 1]), u);
+        y = sb(x);
+        u = f29_reduce_qt(f29_lazy3(y, s1, s2), qt);
+        s1 = f29_reduce_qt(f29_lazy2(s1, u), qt);
+        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);
+        x = r + 2 < rp ? f29_add(f29_lazy2(y, itl[r + 2]), u) : f29_add(y, u);
+    }
+    if (r < rp) {
+        const F29 y = sb(x);
+        const F29 u = f29_reduce_qt(f29_lazy3(y, s1, s2), qt);
+        s1 = f29_reduce_qt(f29_lazy2(s1, u), qt);
+        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);
+        x = f29_add(y, u);
+    }
+    return x;
+}
+
 // ---- pair-cooperative permutation, for levels of 16K..32K states: a quad per
 // state would put two waves on a SIMD, one lane per state leaves half the SIMDs
 // idle.  The even lane of a pair computes S-box 0, the odd lane S-box 1, both
@@ -180,13 +218,7 @@ __device__ __forceinline__ void permute3_f29_pair(F29& s0, F29& s1, F29& s2, con
     F29 x = rp ? f29_add(f29_lazy2(s0, itl[0]), t) : f29_add(s0, t);
     s1 = f29_reduce_qt(f29_lazy2(s1, t), qt);
     s2 = f29_reduce_qt(f29_lazy2(s2, t), qt);
-    for (uint32_t r = 0; r < rp; ++r) {
-        const F29 y = sbox29_coop<D, 2>(x);
-        const F29 u = f29_reduce_qt(f29_lazy3(y, s1, s2), qt);
-        s1 = f29_reduce_qt(f29_lazy2(s1, u), qt);
-        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);
-        x = r + 1 < rp ? f29_add(f29_lazy2(y, itl[r + 1]), u) : f29_add(y, u);
-    }
+    x = partial_rounds_f29<D, 2>(x, s1, s2, itl, rp, qt);
     s0 = x;
     t = f29_zero();
     for (uint32_t r = 0; r < half; ++r) t = full_round_pair<D>(s0, s1, s2, t, ter + 3 * r, odd);
@@ -208,13 +240,7 @@ __device__ __forceinline__ void permute3_f29_coop(F29& s0, F29& s1, F29& s2, con
     F29 x = rp ? f29_add(f29_lazy2(s0, itl[0]), t) : f29_add(s0, t);
     s1 = f29_reduce_qt(f29_lazy2(s1, t), qt);  // < 38.8 r, limbs < 2^31
     s2 = f29_reduce_qt(f29_lazy2(s2, t), qt);
-    for (uint32_t r = 0; r < rp; ++r) {
-        const F29 y = sbox29_coop<D>(x);
-        const F29 u = f29_reduce_qt(f29_lazy3(y, s1, s2), qt);  // < 13.7 r
-        s1 = f29_reduce_qt(f29_lazy2(s1, u), qt);
-        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);
-        x = r + 1 < rp ? f29_add(f29_lazy2(y, itl[r + 1]), u) : f29_add(y, u);
-    }
+    x = partial_rounds_f29<D, 4>(x, s1, s2, itl, rp, qt);
     s0 = x;
     t = f29_zero();
     for (uint32_t r = 0; r < half; ++r) t = full_round_coop<D>(s0, s1, s2, t, ter + 3 * r, j);

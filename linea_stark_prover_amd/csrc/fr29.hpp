@@ -328,11 +328,13 @@ __device__ __forceinline__ F29 f29_from_fr(const Fr& x) {
     return f29_reduce(o);
 }
 
-// F29 -> canonical ark-ff Montgomery words: times 2^-5 (product by 2^256 mod r), reduce to [0, r)
+// F29 -> canonical ark-ff Montgomery words: times 2^-5 (product by 2^256 mod r), reduce to [0, r).
+// Any normalised x < 2^261 is a valid operand (product < x c / 2^261 + 8r + 1 < 9r + 1), so
+// no reduction before the product.
 __device__ __forceinline__ Fr f29_to_fr(const F29& x) {
     const F29 c = f29_const(0x1ffffff3u, 0x8e3ffffu, 0x1ffffc9fu, 0xfea1edfu, 0xfee725u, 0xabaa896u, 0xa745b60u,
                             0x6457773u, 0xd4bdau);
-    const F29 y = f29_reduce(f29_mul(f29_reduce(x), c));  // < 2 r
+    const F29 y = f29_reduce(f29_mul(x, c));  // < 2 r
     return fr_reduce_once(f29_repack_out(y));
 }
 

@@ -143,17 +143,26 @@ struct TileLds {
 // limbs < 2^31 and column sums < 2^63.74 in the product by wB
 // (tools/gen_fr29mul.py --bound), and f29_reduce takes it as it is (its
 // quotient estimate from the top limb still leaves < 2r).
+// the reductions of a group: f29_reduce, or with a per-workgroup LDS table of
+// q r (f29_reduce_qt: 3 plain 32-bit ops per limb instead of 64-bit
+// multiply-adds and shifts) when qt is given.  Every reduced sum below is
+// < 64 r with limbs < 2^31 (the table's biased limb sums stay in [0, 2^32)
+// up to limbs of 3 2^30; its top-limb quotient estimate leaves < 2r as f29_reduce's).
+__device__ __forceinline__ F29 red(const F29& v, const uint4* __restrict__ qt) {
+    return qt ? f29_reduce_qt(v, qt) : f29_reduce(v);
+}
+
 __device__ __forceinline__ void dif4(F29& v0, F29& v1, F29& v2, F29& v3, const F29& wA, const F29& wA2,
-                                     const F29& wB, bool trivB) {
+                                     const F29& wB, bool trivB, const uint4* __restrict__ qt) {
     const F29 u0 = f29_lazy2(v0, v2);                  // < 16.6 r, limbs < 2^30
     const F29 u2 = f29_mul(f29_sub16(v0, v2), wA);    // < 8.06 r
     const F29 u1 = f29_norm(f29_lazy2(v1, v3));
     const F29 u3 = f29_mul(f29_sub16(v1, v3), wA2);
-    v0 = f29_reduce(f29_lazy2(u0, u1));               // < 2 r
-    v2 = f29_reduce(f29_lazy2(u2, u3));
+    v0 = red(f29_lazy2(u0, u1), qt);                  // < 2 r
+    v2 = red(f29_lazy2(u2, u3), qt);
     if (trivB) {
-        v1 = f29_reduce(f29_sub32(u0, u1));
-        v3 = f29_reduce(f29_sub16(u2, u3));
+        v1 = red(f29_sub32(u0, u1), qt);
+        v3 = red(f29_sub16(u2, u3), qt);
     } else {
         v1 = f29_mul(f29_sub32(u0, u1), wB);          // < 48.6 r in -> < 8.11 r
         v3 = f29_mul(f29_sub16(u2, u3), wB);
@@ -164,7 +173,7 @@ __device__ __forceinline__ void dif4(F29& v0, F29& v1, F29& v2, F29& v3, const F
 // t0 + 2d, t0 + 3d: wA = w(s, t0) (= w(s, t0 + 2d)), wB = w(s + 1, t0),
 // wB2 = w(s + 1, t0 + d); trivA: stage s is the transform's first (w = 1).
 __device__ __forceinline__ void dit4(F29& v0, F29& v1, F29& v2, F29& v3, const F29& wA, const F29& wB,
-                                     const F29& wB2, bool trivA) {
+                                     const F29& wB2, bool trivA, const uint4* __restrict__ qt) {
     const F29 p1 = trivA ? v1 : f29_mul(v1, wA);      // < 8.3 r
     const F29 p3 = trivA ? v3 : f29_mul(v3, wA);
     const F29 u0 = f29_lazy2(v0, p1);                 // limbs < 2^30, < 16.6 r
@@ -173,10 +182,10 @@ __device__ __forceinline__ void dit4(F29& v0, F29& v1, F29& v2, F29& v3, const F
     const F29 u3 = f29_sub16(v2, p3);
     const F29 q2 = f29_mul(u2, wB);                   // < 8.07 r
     const F29 q3 = f29_mul(u3, wB2);
-    v0 = f29_reduce(f29_lazy2(u0, q2));               // < 2 r
-    v2 = f29_reduce(f29_sub16(u0, q2));
-    v1 = f29_reduce(f29_lazy2(u1, q3));
-    v3 = f29_reduce(f29_sub16(u1, q3));
+    v0 = red(f29_lazy2(u0, q2), qt);                  // < 2 r
+    v2 = red(f29_sub16(u0, q2), qt);
+    v1 = red(f29_lazy2(u1, q3), qt);
+    v3 = red(f29_sub16(u1, q3), qt);                  // limbs < 2.42 2^30
 }
 
 // One tile: 2^k positions x 2^logG groups x 2^LOGCW columns (power-of-two
@@ -234,7 +243,7 @@ __device__ __forceinline__ uint32_t twl_index(const TileGeom<LOGCW>& gm, uint32_
 template <bool DIF, int LOGCW>
 __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOGCW>& gm, const uint4* __restrict__ tw,
                                             uint32_t s0, uint32_t logH, uint32_t n_el,
-                                            const uint4* twl = nullptr) {
+                                            const uint4* twl = nullptr, const uint4* qt = nullptr) {
     constexpr uint32_t CW = 1u << LOGCW;
     const uint32_t k = gm.k, G = 1u << gm.logG;
     const uint32_t cshift = gm.logG + LOGCW;  // element index = (t << cshift) + (g << LOGCW) + c
@@ -264,9 +273,9 @@ __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOG
             F29 v0 = T.get(e0), v1 = T.get(e0 + de), v2 = T.get(e0 + 2 * de), v3 = T.get(e0 + 3 * de);
             const uint32_t r0 = gm.row_of(t0, g), dr = (1u << b) << gm.logL;
             if (DIF)
-                dif4(v0, v1, v2, v3, tw_at(r0, s), tw_at(r0 + dr, s), triv ? v0 : tw_at(r0, s + 1), triv);
+                dif4(v0, v1, v2, v3, tw_at(r0, s), tw_at(r0 + dr, s), triv ? v0 : tw_at(r0, s + 1), triv, qt);
             else
-                dit4(v0, v1, v2, v3, triv ? v0 : tw_at(r0, s), tw_at(r0, s + 1), tw_at(r0 + dr, s + 1), triv);
+                dit4(v0, v1, v2, v3, triv ? v0 : tw_at(r0, s), tw_at(r0, s + 1), tw_at(r0 + dr, s + 1), triv, qt);
             T.put(e0, v0);
             T.put(e0 + de, v1);
             T.put(e0 + 2 * de, v2);
@@ -287,18 +296,18 @@ __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOG
             const uint32_t a0 = (t0 << cshift) + (g << LOGCW) + c, a1 = a0 + ((1u << logd) << cshift);
             const F29 a = T.get(a0), b = T.get(a1);
             if (trivial) {
-                T.put(a0, f29_reduce(f29_lazy2(a, b)));
-                T.put(a1, f29_reduce(f29_sub16(a, b)));
+                T.put(a0, red(f29_lazy2(a, b), qt));
+                T.put(a1, red(f29_sub16(a, b), qt));
                 continue;
             }
             const F29 wv = tw_at(gm.row_of(t0, g), s);
             if (DIF) {
-                T.put(a0, f29_reduce(f29_lazy2(a, b)));
+                T.put(a0, red(f29_lazy2(a, b), qt));
                 T.put(a1, f29_mul(f29_sub16(a, b), wv));
             } else {
                 const F29 bw = f29_mul(b, wv);
-                T.put(a0, f29_reduce(f29_lazy2(a, bw)));
-                T.put(a1, f29_reduce(f29_sub16(a, bw)));
+                T.put(a0, red(f29_lazy2(a, bw), qt));
+                T.put(a1, red(f29_sub16(a, bw), qt));
             }
         }
         __syncthreads();
@@ -332,6 +341,17 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
     const uint32_t n_el = (K << logG) << LOGCW;
     const TileGeom<LOGCW> gm{p.k, logG, p.logL, tile << logG};
     const TileLds T{lds_raw, lds_raw + n_el, reinterpret_cast<uint32_t*>(lds_raw + 2 * n_el)};
+    // the reduction table after the tile (3 KiB; not in the fused pass, whose
+    // LDS already limits it to 2 workgroups per CU); published by the barrier
+    // after the tile's load below
+    const uint4* qt = nullptr;
+#ifndef LSP_NTT_NO_QT  // A/B switch (tools/variant_lib.py): f29_reduce everywhere
+    if constexpr (!FWD_FIRST) {
+        uint4* q = reinterpret_cast<uint4*>(T.c + n_el);
+        f29_qtab_init(q);
+        qt = q;
+    }
+#endif
     constexpr uint32_t NREG = FWD_FIRST ? NTT_MAX_EL / NTT_THREADS : 1;
     F29 xr[NREG];
     // the forward twiddles of this tile in LDS (after the tile and the per-row
@@ -424,7 +444,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
             }
         }
         __syncthreads();
-        tile_stages<DIF, LOGCW>(T, gm, p.tw, p.s0, p.logH, n_el, twl);
+        tile_stages<DIF, LOGCW>(T, gm, p.tw, p.s0, p.logH, n_el, twl, qt);
         // ---- store
         const bool canon = p.canon != 0;
         for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
@@ -566,6 +586,7 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
         const size_t twl_n = (size_t(1) << logG) * ((size_t(1) << k) - 1);
         p.twl_n = (mode == PASS_INV_FWD && twl_n <= 512 && twl_env) ? (uint32_t)twl_n : 0u;
         lds += (size_t)p.twl_n * 3 * sizeof(uint4);
+        if (mode != PASS_INV_FWD) lds += (size_t)F29_QTAB_N * 3 * sizeof(uint4);  // k_ntt_rm's reduction table
         p.xcd = (tiles / nchunk) % 8 == 0 ? 1u : 0u;
         const dim3 grid((unsigned)tiles), blk(256);
 #define LSP_NTT_LAUNCH(DIFV, MODEV)                                                                   \

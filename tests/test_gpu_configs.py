@@ -11,6 +11,7 @@ pytestmark = pytest.mark.gpu
 CASES = [
     dict(sbox_degree=17),
     dict(rounds_f=4, rounds_p=10),
+    dict(rounds_f=6, rounds_p=7),  # odd: the partial rounds run in pairs plus a last single one
     dict(public_degree=0),
     dict(log_blowup=2, log_final_poly_len=1, num_queries=7),
     dict(log_blowup=4, log_final_poly_len=2, num_queries=50),
@@ -55,6 +56,23 @@ def test_config_matches_oracle(oracle_lib, kw, log_n, ncols):
             off = 8 + 20 + 64 + 32 * (2 * (2 * ncols + 2) + q) + 32 * nr + 32  # second final coefficient
             bad[off] ^= 1
             assert not ctx.verify(bytes(bad), permutation_air(ncols), pub)
+
+
+def test_odd_partial_rounds_every_lane_width(oracle_lib):
+    """rounds_p odd at 2^13 rows: the LDE's 2^16 leaves take the one-state-per-lane
+    kernels, the 32K level the lane-pair one and the narrower levels the quad one,
+    each with the pairwise partial rounds and their single last round."""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import Context, StarkConfig
+    perm = dict(rounds_f=8, rounds_p=23)
+    p = oracle_lib.setup(**perm)
+    log_n, ncols = 13, 3
+    tb, w = oracle_lib.gen_perm_trace(p, log_n, ncols)
+    trace = np.frombuffer(tb.raw, dtype=np.uint64).reshape(1 << log_n, w, 4).copy()
+    pub = np.concatenate([np.array(p.alpha, np.uint64).reshape(1, 4), np.array(p.delta, np.uint64).reshape(1, 4)])
+    with Context(StarkConfig(**perm)) as ctx:
+        got = ctx.prove(trace, permutation_air(ncols), pub)
+    assert got == oracle_lib.prove(p, trace.ctypes.data, 1 << log_n, w, oracle_lib.perm_air(ncols))
 
 
 def test_sharded_with_small_blowup(gpu_ctx):

@@ -41,7 +41,7 @@ kern = [k for k in sorted(fetch) if lo <= k <= hi and 'copyBuffer' not in fetch[
 fb = sum(fetch[k][1] for k in kern) * 1024 * 2
 wb = sum(write[k][1] for k in kern if k in write) * 1024
 alg = 32 * w * (h + (h << added))
-res = {"kernel": "coset_lde_batch (twist tables, 3 row-major DIT passes, 3 row-major DIF passes with fused twist)",
+res = {"kernel": "coset_lde_batch (row-major: inverse DIT pass(es), the fused inverse-last / twisted forward-first pass, in-place forward DIF pass(es))",
        "h": h, "w": w, "fetch_bytes": fb, "write_bytes": wb, "traffic_bytes": fb + wb,
        "algorithmic_bytes": alg, "traffic_over_algorithmic": (fb + wb) / alg,
        "per_kernel": [{"dispatch": k, "kernel": fetch[k][0].replace('lsp::(anonymous namespace)::', '').replace('void ', '').split('(')[0],

@@ -530,9 +530,15 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
     // (k = 9: CW = 2, ..., k <= 7: CW = 8), and the narrow row accesses are
     // merged in L2 by the XCD-aware tile order.  LSP_NTT_LOGCW (minimum column
     // chunk) / LSP_NTT_KMAX override (LOGCW=3 KMAX=7: the r01 shape).
-    static const uint32_t logcw_env = [] {  // minimum log2 column chunk (bounds k)
+    // minimum log2 column chunk (bounds k).  Narrow chunks rely on the XCD's L2
+    // holding a tile's rows until all its chunks have read them; from ~48
+    // columns (1.5 MiB per 1024-row tile) that stops working, and passes of
+    // whole 256-byte row segments win: 2^20 x 184 172.6 -> 161.5 ms, 2^19 x 64
+    // 27.8 -> 27.4 ms; at 8..32 columns the 2-pass plan stays ahead (2^19 x 14
+    // 6.0 against 7.0 ms) -- tools/sweep_lde_logcw.sh, profiles/r02u_lde_logcw.txt
+    static const int logcw_env = [] {
         const char* e = std::getenv("LSP_NTT_LOGCW");
-        return e ? (uint32_t)std::min(3, std::max(0, std::atoi(e))) : 0u;
+        return e ? std::min(3, std::max(0, std::atoi(e))) : -1;
     }();
     static const bool twl_env = [] {  // LSP_NTT_TWL=0: the fused pass reads its twiddles from HBM
         const char* e = std::getenv("LSP_NTT_TWL");
@@ -544,7 +550,8 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
     }();
     uint32_t logCWmax = 0;  // the power of two >= min(w, 8)
     while ((1u << logCWmax) < w && logCWmax < 3) ++logCWmax;
-    const uint32_t kmax = std::min(kmax_env, 10 - std::min(logCWmax, logcw_env));
+    const uint32_t logcw_min = logcw_env >= 0 ? (uint32_t)logcw_env : (w >= 48 ? 1u : 0u);
+    const uint32_t kmax = std::min(kmax_env, 10 - std::min(logCWmax, logcw_min));
     uint32_t ks[16], np;
     plan_passes(logh, kmax, ks, np);
     // inverse: passes ks[0], ..., ks[np-1] (DIT, stages in increasing order);

@@ -32,9 +32,17 @@ __global__ __launch_bounds__(256) void k_selector_denoms(const Fr* __restrict__ 
 }
 
 __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
-    const size_t m = gtid();
+    const size_t t = gtid();
     const size_t Q = 1ull << a.logQ;
-    if (m >= (a.n ? a.n : Q)) return;
+    if (t >= (a.n ? a.n : Q)) return;  // n = Q >> log_step points
+    // Wide rows: thread t evaluates point m = bitrev(t), whose row bitrev_Q(i)
+    // is row0 + t, so a wave reads 64 adjacent LDE rows (and their
+    // successors).  In point order it read rows Q/64 apart, and with the C3
+    // trace's 5.9 KB rows their lines left the L2 before the lane came back
+    // for the next columns (2^20 x 184: 63.5 -> 36.7 ms).  Narrow rows keep
+    // point order (coalesced inv_den reads and out writes; 2^19 x 8 is ~5 %
+    // faster that way).
+    const size_t m = a.w >= 32 ? brev_bits(t, a.logQ - a.log_step) : t;
     const uint64_t i = a.i0 + ((uint64_t)m << a.log_step);
     const uint32_t qmask = (1u << a.log_q) - 1;
     const Fr one = fr_one();

@@ -40,24 +40,27 @@ __global__ __launch_bounds__(256) void k_interp_partial(const Fr* __restrict__ M
     __shared__ Fr red[256];
     __shared__ Fr sc[INTERP_ROWS];
     const size_t r0 = (size_t)blockIdx.x * INTERP_ROWS;
-    for (uint32_t e = threadIdx.x; e < INTERP_ROWS; e += blockDim.x) {
-        const size_t i = r0 + e;
-        if (i < h) sc[e] = fr_mul(fr_mul(gen, pow2l(tabN, L1, brev_bits(i, logN))), inv_den[i]);
-    }
+    const uint32_t nr = (uint32_t)min((size_t)INTERP_ROWS, h - r0);
+    for (uint32_t e = threadIdx.x; e < nr; e += blockDim.x)
+        sc[e] = fr_mul(fr_mul(gen, pow2l(tabN, L1, brev_bits(r0 + e, logN))), inv_den[r0 + e]);
     __syncthreads();
-    for (uint32_t c = 0; c < w; ++c) {
+    // the threads as R row lanes x W adjacent columns (W = min(w, 256)): one step
+    // reads W adjacent elements of R consecutive rows, a contiguous run of the
+    // row-major matrix; one LDS sum per column chunk instead of a tree per column
+    const uint32_t W = min(w, 256u), R = 256u / W;
+    const uint32_t cc = threadIdx.x % W, rr = threadIdx.x / W;
+    for (uint32_t c0 = 0; c0 < w; c0 += W) {
+        const uint32_t c = c0 + cc;
         Fr acc = fr_zero();
-        for (uint32_t e = threadIdx.x; e < INTERP_ROWS; e += blockDim.x) {
-            const size_t i = r0 + e;
-            if (i < h) acc = fr_add(acc, fr_mul(M[i * w + c], sc[e]));
-        }
+        if (rr < R && c < w)
+            for (uint32_t r = rr; r < nr; r += R) acc = fr_add(acc, fr_mul(M[(r0 + r) * w + c], sc[r]));
         red[threadIdx.x] = acc;
         __syncthreads();
-        for (uint32_t s = 128; s > 0; s >>= 1) {
-            if (threadIdx.x < s) red[threadIdx.x] = fr_add(red[threadIdx.x], red[threadIdx.x + s]);
-            __syncthreads();
+        if (threadIdx.x < W && c0 + threadIdx.x < w) {
+            Fr sum = red[threadIdx.x];
+            for (uint32_t k = 1; k < R; ++k) sum = fr_add(sum, red[threadIdx.x + k * W]);
+            partial[(size_t)blockIdx.x * w + c0 + threadIdx.x] = sum;
         }
-        if (threadIdx.x == 0) partial[(size_t)blockIdx.x * w + c] = red[0];
         __syncthreads();
     }
 }

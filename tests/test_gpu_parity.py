@@ -39,7 +39,8 @@ def c_ptr(a):
 
 # ------------------------------------------------------------------ LDE
 # pass plans (k_ntt.hip, k <= 10 per pass): one fused pass up to 2^10; [6,5] [6,6] [7,6]
-# [7,7] [8,7] [8,8] [9,8] [9,9] above, with the per-pass column chunk and partial chunks
+# [7,7] [8,7] [8,8] [9,8] [9,9] above, with the per-pass column chunk and partial chunks;
+# (the wide plan of 48+ columns: test_coset_lde_wide_plan)
 @pytest.mark.parametrize("logh,w,added", [(1, 1, 1), (3, 2, 3), (5, 8, 3), (8, 14, 3), (10, 4, 2), (12, 8, 3),
                                           (13, 3, 3), (11, 1, 3), (14, 5, 3), (15, 14, 3), (16, 2, 1),
                                           (17, 1, 3), (18, 3, 2)])
@@ -54,6 +55,27 @@ def test_coset_lde_matches_oracle(gpu_ctx, oracle_lib, logh, w, added):
     oracle_lib.lib().lo_coset_lde_batch(c_ptr(mat), ctypes.c_size_t(h), ctypes.c_size_t(w), added, c_ptr(shifts),
                                         c_ptr(exp), 8)
     assert np.array_equal(got, exp)
+
+
+def test_coset_lde_wide_plan(gpu_ctx, oracle_lib):
+    """From 48 columns launch_lde plans 8-column chunks: 2^19 x 50 runs as
+    [7,6,6] (whole 256-byte row segments, a partial last chunk of 2) instead of
+    [10,9].  Columns transform independently, so the oracle checks a few of
+    them, from the first chunk, a chunk boundary and the partial chunk."""
+    rng = np.random.default_rng(1950)
+    logh, w, added = 19, 50, 1
+    h = 1 << logh
+    mat = rng.integers(0, 2**64, size=(h, w, 4), dtype=np.uint64)  # canonical Montgomery words:
+    mat[..., 3] &= (1 << 58) - 1                                   # every value < 2^250 < r
+    shift = rand_fr(rng, (1,))
+    got = gpu_ctx.coset_lde_batch(mat, added, shift)
+    cols = [0, 7, 8, 48, 49]
+    sub = np.ascontiguousarray(mat[:, cols])
+    exp = np.zeros((h << added, len(cols), 4), dtype=np.uint64)
+    shifts = np.repeat(shift.reshape(1, 4), len(cols), axis=0).copy()
+    oracle_lib.lib().lo_coset_lde_batch(c_ptr(sub), ctypes.c_size_t(h), ctypes.c_size_t(len(cols)), added,
+                                        c_ptr(shifts), c_ptr(exp), 16)
+    assert np.array_equal(got[:, cols], exp)
 
 
 def test_coset_lde_per_column_shifts(gpu_ctx, oracle_lib):

@@ -9,13 +9,12 @@
 //     folded into the next S-box input with the round constant: inputs
 //     < 4 Y + 2 inside a permutation (Y = the S-box output bound), < 8 Y + 6
 //     at the start of a sponge permutation (s2 carries over);
-//   partial rounds: u = reduce(y + s1 + s2) < 2 r, s2 = reduce(2 s2 + u),
-//     s1 = s1 + u carry-free in even rounds (limbs < 2^30, < 4 r) and
-//     reduce(s1 + u) in odd ones: limb-wise sums (< 15.7 r, limbs < 2^31)
-//     into the LDS-table reduction f29_reduce_qt (`qt`, valid below 64 r
-//     with limbs < 2.41 2^30), so s2 stays < 2 r and s1 < 4 r for any number
-//     of partial rounds (a lazy s1 enters the terminal full rounds through a
-//     carry-propagating add);
+//   partial rounds: u = y + s1 + s2 carry-free (limbs < 1.5 2^30, < Y + 4 r),
+//     s1 = reduce(s1 + u), s2 = reduce(2 s2 + u): limb-wise sums (< Y + 8 r,
+//     limbs < 2.5 2^30) into the LDS-table reduction f29_reduce_qt (`qt`,
+//     valid below 64 r with limbs below 3 2^30, tests/test_f29_bounds.py), so
+//     s1 and s2 stay < 2 r for any number of partial rounds; the next S-box
+//     input y + c + u (one carry-propagating add) is < 2 Y + 5 r;
 //   the output state is normalised and < 4 Y.
 #pragma once
 #include "fr29.hpp"
@@ -32,9 +31,9 @@ __device__ __forceinline__ F29 sbox29(const F29& x) {
 }
 
 
-// The partial rounds two at a time (no branch inside the pair): s1 carry-free
-// after the first, reduced after the second (header); an odd last round
-// reduces it.  LANES: 1 (one state per lane) or 2 / 4 (cooperative S-box).
+// The partial rounds: the internal layer's sum u stays carry-free and only s1
+// and s2 are reduced (header).  LANES: 1 (one state per lane) or 2 / 4
+// (cooperative S-box).
 template <uint32_t D, int LANES>
 __device__ __forceinline__ F29 partial_rounds_f29(F29 x, F29& s1, F29& s2, const F29* __restrict__ itl, uint32_t rp,
                                                   const uint4* __restrict__ qt);
@@ -159,25 +158,12 @@ __device__ __forceinline__ F29 partial_rounds_f29(F29 x, F29& s1, F29& s2, const
         else
             return sbox29_coop<D, LANES>(v);
     };
-    uint32_t r = 0;
-    for (; r + 2 <= rp; r += 2) {
-        F29 y = sb(x);
-        F29 u = f29_reduce_qt(f29_lazy3(y, s1, s2), qt);
-        s1 = f29_lazy2(s1, u);
-        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);
-        x = f29_add(f29_lazy2(y, itl[r + 1]), u);
-        y = sb(x);
-        u = f29_reduce_qt(f29_lazy3(y, s1, s2), qt);
-        s1 = f29_reduce_qt(f29_lazy2(s1, u), qt);
-        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);
-        x = r + 2 < rp ? f29_add(f29_lazy2(y, itl[r + 2]), u) : f29_add(y, u);
-    }
-    if (r < rp) {
+    for (uint32_t r = 0; r < rp; ++r) {
         const F29 y = sb(x);
-        const F29 u = f29_reduce_qt(f29_lazy3(y, s1, s2), qt);
-        s1 = f29_reduce_qt(f29_lazy2(s1, u), qt);
-        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);
-        x = f29_add(y, u);
+        const F29 u = f29_lazy3(y, s1, s2);              // carry-free: limbs < 1.5 2^30, < Y + 4r
+        s1 = f29_reduce_qt(f29_lazy2(s1, u), qt);       // limbs < 2^31
+        s2 = f29_reduce_qt(f29_lazy3(s2, s2, u), qt);   // limbs < 2.5 2^30
+        x = r + 1 < rp ? f29_add(f29_lazy2(y, itl[r + 1]), u) : f29_add(y, u);  // < 2Y + 5r
     }
     return x;
 }

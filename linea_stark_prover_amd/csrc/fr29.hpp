@@ -309,7 +309,11 @@ __device__ __forceinline__ F29 f29_const(uint32_t l0, uint32_t l1, uint32_t l2, 
 // ark-ff Montgomery (X = x 2^256 mod r, < 2^256) -> F29 (x 2^261): the integer
 // X * 2^5 (< 32 r < 2^261) is already a lazily reduced F29 value, so this is a
 // repack with a 5-bit offset plus one cheap reduction to < 2r -- no product.
-__device__ __forceinline__ F29 f29_from_fr(const Fr& x) {
+__device__ __forceinline__ F29 f29_from_fr_lazy(const Fr& x);
+__device__ __forceinline__ F29 f29_from_fr(const Fr& x) { return f29_reduce(f29_from_fr_lazy(x)); }
+
+// X * 2^5 as F29 limbs, < 32 r, not reduced
+__device__ __forceinline__ F29 f29_from_fr_lazy(const Fr& x) {
     F29 o;
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
@@ -325,7 +329,7 @@ __device__ __forceinline__ F29 f29_from_fr(const Fr& x) {
         }
         o.l[i] = v & (i < 8 ? F29_MASK : 0xffffffffu);
     }
-    return f29_reduce(o);
+    return o;
 }
 
 // F29 -> canonical ark-ff Montgomery words: times 2^-5 (product by 2^256 mod r), reduce to [0, r).
@@ -336,6 +340,16 @@ __device__ __forceinline__ Fr f29_to_fr(const F29& x) {
                             0x6457773u, 0xd4bdau);
     const F29 y = f29_reduce(f29_mul(x, c));  // < 2 r
     return fr_reduce_once(f29_repack_out(y));
+}
+
+// f29_to_fr with the reduction through the LDS table of q r (f29_reduce_qt:
+// 32-bit ops only; identical result; the product is < 9r + 1, so q <= 8) for
+// kernels that hold the table.  (Absorbed inputs keep f29_from_fr: a caller's
+// word may be any value below 2^256, beyond the table's 64 r.)
+__device__ __forceinline__ Fr f29_to_fr_qt(const F29& x, const uint4* __restrict__ qt) {
+    const F29 c = f29_const(0x1ffffff3u, 0x8e3ffffu, 0x1ffffc9fu, 0xfea1edfu, 0xfee725u, 0xabaa896u, 0xa745b60u,
+                            0x6457773u, 0xd4bdau);
+    return fr_reduce_once(f29_repack_out(f29_reduce_qt(f29_mul(x, c), qt)));
 }
 
 }  // namespace lsp

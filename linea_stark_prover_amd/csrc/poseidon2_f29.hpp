@@ -269,7 +269,7 @@ __device__ __forceinline__ Fr sponge_f29(Get get, uint32_t n, const F29* rc29, u
         s0 = f29_from_fr(n0);
         permute3_any<D, LANES>(s0, s1, s2, rc29, rf, rp, qt);
     }
-    return f29_to_fr(s0);
+    return f29_to_fr_qt(s0, qt);
 }
 
 template <uint32_t D, int LANES = 1>
@@ -277,7 +277,7 @@ __device__ __forceinline__ Fr compress_f29(const Fr& l, const Fr& r, const F29* 
                                            const uint4* __restrict__ qt) {
     F29 s0 = f29_from_fr(l), s1 = f29_from_fr(r), s2 = f29_zero();
     permute3_any<D, LANES>(s0, s1, s2, rc29, rf, rp, qt);
-    return f29_to_fr(s0);
+    return f29_to_fr_qt(s0, qt);
 }
 
 }  // namespace lsp

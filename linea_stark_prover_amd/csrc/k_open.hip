@@ -108,24 +108,51 @@ __global__ __launch_bounds__(256) void k_reduce_rows(ReduceArgs a) {
     const size_t i = gtid();
     if (i >= a.n) return;
     const Fr* row = a.lde + i * a.w;
+    const Fr* qrow = a.qlde + i * a.q;
+    // Software-pipelined loads: the next chunk of the row (then of the quotient
+    // row) is requested before the current chunk's products, so a wave waits
+    // for HBM about once per row instead of once per element (the loads used to
+    // sit right before their products, ~1/3 of the kernel's cycles stalled).
+    constexpr uint32_t RC = RR_CHUNK;
+    auto load = [&](const Fr* p, uint32_t n, uint32_t k, Fr* dst) {
+#pragma unroll
+        for (uint32_t j = 0; j < RC; ++j)
+            if (k + j < n) dst[j] = p[k + j];
+    };
+    const Fr zi = a.inv_z[i], zni = a.inv_zn[i];
+    Fr cur[RC], nxt[RC];
+    if (a.w)
+        load(row, a.w, 0, cur);
+    else
+        load(qrow, a.q, 0, cur);
     F29 rr = f29_zero();
-    for (uint32_t k = 0; k < a.w; k += RR_CHUNK) {
+    for (uint32_t k = 0; k < a.w; k += RC) {
+        if (k + RC < a.w)
+            load(row, a.w, k + RC, nxt);
+        else
+            load(qrow, a.q, 0, nxt);  // the quotient row's first chunk
         F29 s = rr;
-        const uint32_t e = min(a.w, k + RR_CHUNK);
-        for (uint32_t c = k; c < e; ++c) s = f29_lazy2(s, f29_mul(f29_repack_in(row[c]), apw29[c]));  // < 8.06 r each
+#pragma unroll
+        for (uint32_t j = 0; j < RC; ++j)
+            if (k + j < a.w) s = f29_lazy2(s, f29_mul(f29_repack_in(cur[j]), apw29[k + j]));  // < 8.06 r each
         rr = f29_reduce_qt(s, qt);  // < 2 r
+#pragma unroll
+        for (uint32_t j = 0; j < RC; ++j) cur[j] = nxt[j];
     }
-    const F29 iz = f29_from_fr(a.inv_z[i]), izn = f29_from_fr(a.inv_zn[i]);  // 29-bit form, < 2 r
+    const F29 iz = f29_from_fr(zi), izn = f29_from_fr(zni);  // 29-bit form, < 2 r
     const F29 t1 = f29_mul(f29_sub16(f29_repack_in(a.ry_z), rr), iz);          // < 17 r in, < 8.1 r out
     const F29 t2 = f29_mul(f29_mul(f29_sub16(f29_repack_in(a.ry_zn), rr), izn), apw29[a.w]);
-    const Fr* qrow = a.qlde + i * a.q;
     F29 qacc = f29_zero();
-    for (uint32_t k = 0; k < a.q; k += RR_CHUNK) {
+    for (uint32_t k = 0; k < a.q; k += RC) {
+        if (k + RC < a.q) load(qrow, a.q, k + RC, nxt);
         F29 s = qacc;
-        const uint32_t e = min(a.q, k + RR_CHUNK);
-        for (uint32_t j = k; j < e; ++j)
-            s = f29_lazy2(s, f29_mul(f29_sub16(ryq_l[j], f29_repack_in(qrow[j])), apw29[a.w + 1 + j]));
+#pragma unroll
+        for (uint32_t j = 0; j < RC; ++j)
+            if (k + j < a.q)
+                s = f29_lazy2(s, f29_mul(f29_sub16(ryq_l[k + j], f29_repack_in(cur[j])), apw29[a.w + 1 + k + j]));
         qacc = f29_reduce_qt(s, qt);
+#pragma unroll
+        for (uint32_t j = 0; j < RC; ++j) cur[j] = nxt[j];
     }
     const F29 t3 = f29_mul(qacc, iz);
     a.out[i] = fr_reduce_once(f29_repack_out(f29_reduce_qt(f29_lazy3(t1, t2, t3), qt)));  // < 24.3 r in

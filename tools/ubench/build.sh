@@ -7,7 +7,7 @@ HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 names=${*:-"rates p2bench mulbench"}
 for n in $names; do
     case $n in
-        host_perm) g++ -O3 -march=native -std=c++17 -o host_perm_bin host_perm.cpp ;;
+        host_perm) $HIPCC --cuda-host-only -O3 -march=native -std=c++17 -I../../linea_stark_prover_amd/csrc -o host_perm_bin host_perm.cpp ;;
         *) $HIPCC --offload-arch=gfx950 -O3 -std=c++17 -o "$n" "$n.hip" ;;
     esac
 done

@@ -8,42 +8,89 @@ namespace lsp {
 
 namespace {
 // Batch inversion, hierarchical (Montgomery's trick at every level):
-//   up    thread t owns elements t, t+T, t+2T, ... (`chunk` of them, interleaved
-//         so every pass is coalesced): out[i] = prefix product before i, and
-//         prod[t] = the chunk's product;
-//   the T chunk products are inverted the same way, recursively, down to a
+//   up    workgroup b owns the 4096 elements [4096 b, 4096 b + 4096): thread t
+//         the 16 elements 4096 b + 256 j + t (every pass coalesced), whose
+//         prefix products it writes to out[]; the 256 chunk products go up a
+//         product tree in LDS and prod[b] = the workgroup's product;
+//   the workgroup products are inverted the same way, recursively, down to a
 //   base of <= BI_BASE elements that one workgroup inverts with a product
-//   tree in LDS and ONE Fermat inverse (on the 29-bit multiplier);
-//   down  thread t walks its chunk backwards from 1/prod[t].
-// Cost ~3 products per element plus one inversion for the whole batch; the
-// critical path is a few short chains plus that one inversion.
-constexpr uint32_t BI_CHUNK = 16;
+//   tree in LDS and ONE Fermat inverse (on the 29-bit multiplier) -- skipped
+//   when the caller knows the inverse of the whole product;
+//   down  workgroup b rebuilds its tree (a thread's chunk product is its last
+//         prefix times its last element), takes 1/prod[b] down the tree and
+//         walks every chunk backwards.
+// Cost ~3 products per element plus one inversion for the whole batch; one
+// level per 4096x (2^22 elements: up, base, down -- three launches; the
+// per-thread chains of the earlier 16x levels took seven).
 constexpr uint32_t BI_THREADS = 256;
+constexpr uint32_t BI_CHUNK = 16;
+constexpr uint32_t BI_WG = BI_THREADS * BI_CHUNK;  // elements per workgroup of the up/down passes
 constexpr uint32_t BI_BASE = BI_THREADS * 16;
 
-__global__ __launch_bounds__(256) void k_bi_up(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n, size_t T,
-                                               uint32_t chunk, Fr* __restrict__ prod) {
-    const size_t t = gtid();
-    if (t >= T) return;
+// the product tree of a workgroup's 256 chunk products (node k: children 2k,
+// 2k+1; leaves at BI_THREADS + t); ends with a barrier
+__device__ __forceinline__ void bi_tree_up(Fr* tree, uint32_t t, const Fr& acc) {
+    tree[BI_THREADS + t] = acc;
+    __syncthreads();
+    for (uint32_t w = BI_THREADS / 2; w >= 1; w >>= 1) {
+        if (t < w) tree[w + t] = fr_mul(tree[2 * (w + t)], tree[2 * (w + t) + 1]);
+        __syncthreads();
+    }
+}
+
+// tree[1] = 1/(the root's product) on entry; afterwards node k holds 1/(its
+// subtree's product), so leaf BI_THREADS + t is 1/(chunk t's product)
+__device__ __forceinline__ void bi_tree_down(Fr* tree, uint32_t t) {
+    for (uint32_t w = 1; w < BI_THREADS; w <<= 1) {
+        Fr l, r;
+        if (t < w) {
+            const Fr iv = tree[w + t];
+            l = fr_mul(iv, tree[2 * (w + t) + 1]);
+            r = fr_mul(iv, tree[2 * (w + t)]);
+        }
+        __syncthreads();
+        if (t < w) {
+            tree[2 * (w + t)] = l;
+            tree[2 * (w + t) + 1] = r;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(BI_THREADS) void k_bi_up(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n,
+                                                      Fr* __restrict__ prod) {
+    __shared__ Fr tree[2 * BI_THREADS];
+    const uint32_t t = threadIdx.x;
+    const size_t base = (size_t)blockIdx.x * BI_WG + t;
     Fr acc = fr_one();
-    for (uint32_t j = 0; j < chunk; ++j) {
-        const size_t i = t + (size_t)j * T;
+    for (uint32_t j = 0; j < BI_CHUNK; ++j) {
+        const size_t i = base + (size_t)j * BI_THREADS;
         if (i >= n) break;
         out[i] = acc;
         acc = fr_mul(acc, in[i]);
     }
-    prod[t] = acc;
+    bi_tree_up(tree, t, acc);
+    if (t == 0) prod[blockIdx.x] = tree[1];
 }
 
-__global__ __launch_bounds__(256) void k_bi_down(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n, size_t T,
-                                                 uint32_t chunk, const Fr* __restrict__ inv_prod) {
-    const size_t t = gtid();
-    if (t >= T) return;
-    Fr inv = inv_prod[t];
-    uint32_t cnt = 0;
-    while (cnt < chunk && t + (size_t)cnt * T < n) ++cnt;
+__global__ __launch_bounds__(BI_THREADS) void k_bi_down(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n,
+                                                        const Fr* __restrict__ inv_prod) {
+    __shared__ Fr tree[2 * BI_THREADS];
+    const uint32_t t = threadIdx.x;
+    const size_t base = (size_t)blockIdx.x * BI_WG + t;
+    const uint32_t cnt = base >= n ? 0u : (uint32_t)min((size_t)BI_CHUNK, (n - 1 - base) / BI_THREADS + 1);
+    Fr acc = fr_one();
+    if (cnt) {
+        const size_t il = base + (size_t)(cnt - 1) * BI_THREADS;
+        acc = fr_mul(out[il], in[il]);  // the chunk's product: its last prefix times its last element
+    }
+    bi_tree_up(tree, t, acc);
+    if (t == 0) tree[1] = inv_prod[blockIdx.x];
+    __syncthreads();
+    bi_tree_down(tree, t);
+    Fr inv = tree[BI_THREADS + t];
     for (uint32_t j = cnt; j-- > 0;) {
-        const size_t i = t + (size_t)j * T;
+        const size_t i = base + (size_t)j * BI_THREADS;
         const Fr o = fr_mul(inv, out[i]);
         inv = fr_mul(inv, in[i]);
         out[i] = o;
@@ -80,29 +127,10 @@ __global__ __launch_bounds__(BI_THREADS) void k_bi_base(const Fr* __restrict__ i
         out[i] = acc;
         acc = fr_mul(acc, in[i]);
     }
-    tree[BI_THREADS + t] = acc;
-    __syncthreads();
-    for (uint32_t w = BI_THREADS / 2; w >= 1; w >>= 1) {
-        if (t < w) tree[w + t] = fr_mul(tree[2 * (w + t)], tree[2 * (w + t) + 1]);
-        __syncthreads();
-    }
+    bi_tree_up(tree, t, acc);
     if (t == 0) tree[1] = have_inv ? inv_total : fr_inv_f29(tree[1]);
     __syncthreads();
-    // top-down: node k holds 1/(product of its subtree); children swap products
-    for (uint32_t w = 1; w < BI_THREADS; w <<= 1) {
-        Fr l, r;
-        if (t < w) {
-            const Fr iv = tree[w + t];
-            l = fr_mul(iv, tree[2 * (w + t) + 1]);
-            r = fr_mul(iv, tree[2 * (w + t)]);
-        }
-        __syncthreads();
-        if (t < w) {
-            tree[2 * (w + t)] = l;
-            tree[2 * (w + t) + 1] = r;
-        }
-        __syncthreads();
-    }
+    bi_tree_down(tree, t);
     Fr inv = tree[BI_THREADS + t];
     if (t >= n) return;
     const size_t last = t + ((n - 1 - t) / BI_THREADS) * BI_THREADS;
@@ -176,7 +204,7 @@ __global__ __launch_bounds__(256) void k_assemble_chunks(const Fr* __restrict__ 
 size_t batch_inverse_scratch(size_t n) {
     size_t tot = 0;
     while (n > BI_BASE) {
-        n = (n + BI_CHUNK - 1) / BI_CHUNK;
+        n = (n + BI_WG - 1) / BI_WG;
         tot += 2 * n;
     }
     return tot;
@@ -197,15 +225,15 @@ hipError_t launch_batch_inverse(const Fr* in, Fr* out, size_t n, hipStream_t st,
                            inv_total ? 1 : 0);
         return hipGetLastError();
     }
-    const size_t T = (n + BI_CHUNK - 1) / BI_CHUNK;
+    const size_t T = (n + BI_WG - 1) / BI_WG;  // workgroups of the up/down passes = products one level up
     Fr* prod = scratch;
     Fr* inv_prod = scratch + T;
-    hipLaunchKernelGGL(k_bi_up, dim3(nblocks(T, 256)), dim3(256), 0, st, in, out, n, T, BI_CHUNK, prod);
+    hipLaunchKernelGGL(k_bi_up, dim3((unsigned)T), dim3(BI_THREADS), 0, st, in, out, n, prod);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     e = launch_batch_inverse(prod, inv_prod, T, st, scratch + 2 * T, inv_total);  // same total product
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_bi_down, dim3(nblocks(T, 256)), dim3(256), 0, st, in, out, n, T, BI_CHUNK, inv_prod);
+    hipLaunchKernelGGL(k_bi_down, dim3((unsigned)T), dim3(BI_THREADS), 0, st, in, out, n, inv_prod);
     return hipGetLastError();
 }
 

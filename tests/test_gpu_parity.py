@@ -191,7 +191,7 @@ def test_fri_fold_matches_pyoracle_and_fold_row(gpu_ctx, logn):
 
 
 # ----------------------------------------------------------- batch inverse
-@pytest.mark.parametrize("n", [1, 31, 32, 33, 1000, 4096, 4097, 70001, (1 << 20) + 3])
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 1000, 4096, 4097, 8191, 8192, 70001, (1 << 20) + 3, (1 << 24) + 4097])
 def test_batch_inverse(gpu_ctx, n):
     """hierarchical Montgomery trick: one-workgroup base (n <= 4096), one and
     several up/down levels above it"""

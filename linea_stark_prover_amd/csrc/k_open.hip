@@ -33,16 +33,23 @@ __global__ __launch_bounds__(256) void k_shift_inverse(const Fr* __restrict__ in
 constexpr uint32_t INTERP_ROWS = 1024;  // rows per block
 
 // partial[b*w + c] = sum over the block's rows i of M[i][c] * x_i * inv_den[i]
+// The row factors x_i inv_den[i] go into LDS once per block in the 29-bit form,
+// so every M[i][c] (ark form) times its factor is the 29-bit product (ark form
+// out, as in k_reduce_rows), accumulated lazily and reduced every RR_CHUNK
+// products through the LDS table; the column sums leave canonical.
+constexpr uint32_t RR_CHUNK = 3;  // 3 normalised products + a value < 2r: limbs < 2^31, < 26.2 r (f29_reduce_qt)
 __global__ __launch_bounds__(256) void k_interp_partial(const Fr* __restrict__ M, uint32_t w, size_t h,
                                                         const Fr* __restrict__ inv_den, Fr gen,
                                                         const Fr* __restrict__ tabN, uint32_t L1, uint32_t logN,
                                                         Fr* __restrict__ partial) {
     __shared__ Fr red[256];
-    __shared__ Fr sc[INTERP_ROWS];
+    __shared__ F29 sc[INTERP_ROWS];
+    __shared__ uint4 qt[3 * F29_QTAB_N];
+    f29_qtab_init(qt);
     const size_t r0 = (size_t)blockIdx.x * INTERP_ROWS;
     const uint32_t nr = (uint32_t)min((size_t)INTERP_ROWS, h - r0);
     for (uint32_t e = threadIdx.x; e < nr; e += blockDim.x)
-        sc[e] = fr_mul(fr_mul(gen, pow2l(tabN, L1, brev_bits(r0 + e, logN))), inv_den[r0 + e]);
+        sc[e] = f29_from_fr(fr_mul(fr_mul(gen, pow2l(tabN, L1, brev_bits(r0 + e, logN))), inv_den[r0 + e]));
     __syncthreads();
     // the threads as R row lanes x W adjacent columns (W = min(w, 256)): one step
     // reads W adjacent elements of R consecutive rows, a contiguous run of the
@@ -52,8 +59,18 @@ __global__ __launch_bounds__(256) void k_interp_partial(const Fr* __restrict__ M
     for (uint32_t c0 = 0; c0 < w; c0 += W) {
         const uint32_t c = c0 + cc;
         Fr acc = fr_zero();
-        if (rr < R && c < w)
-            for (uint32_t r = rr; r < nr; r += R) acc = fr_add(acc, fr_mul(M[(r0 + r) * w + c], sc[r]));
+        if (rr < R && c < w) {
+            F29 s = f29_zero();
+            uint32_t k = 0;
+            for (uint32_t r = rr; r < nr; r += R) {
+                s = f29_lazy2(s, f29_mul(f29_repack_in(M[(r0 + r) * w + c]), sc[r]));  // < 8.06 r each
+                if (++k == RR_CHUNK) {
+                    s = f29_reduce_qt(s, qt);  // < 2 r
+                    k = 0;
+                }
+            }
+            acc = fr_reduce_once(f29_repack_out(f29_reduce_qt(s, qt)));
+        }
         red[threadIdx.x] = acc;
         __syncthreads();
         if (threadIdx.x < W && c0 + threadIdx.x < w) {
@@ -89,7 +106,6 @@ __global__ __launch_bounds__(256) void k_sum_partials(const Fr* __restrict__ par
 // per-row factor (the inverse denominators) once per row; sums stay lazily
 // reduced (at most 3 products per limb-wise sum, then the LDS-table
 // reduction).  The result is canonical.
-constexpr uint32_t RR_CHUNK = 3;  // 3 normalised products + a value < 2r: limbs < 2^31, < 26.2 r (f29_reduce_qt)
 __global__ __launch_bounds__(256) void k_reduce_rows(ReduceArgs a) {
     extern __shared__ uint4 rr_lds[];
     uint4* qt = rr_lds;                                               // 3 * F29_QTAB_N

@@ -8,16 +8,35 @@
 // constraint order of eval.  Row `local` is LDE row bitrev_Q(i) and `next`
 // is bitrev_Q((i + 2^log_q) mod Q) (get_evaluations_on_domain +
 // vertically_packed_row_pair).
+#include "fr29.hpp"
 #include "k_common.hpp"
 #include "kernels.hpp"
 
 namespace lsp {
 
 namespace {
-__device__ __forceinline__ Fr horner(const Fr* __restrict__ row, const int32_t* __restrict__ ids, int32_t n,
-                                     const Fr& a) {
-    Fr acc = fr_zero();
-    for (int32_t k = 0; k < n; ++k) acc = fr_add(fr_mul(acc, a), row[ids[k]]);
+// The constraint arithmetic runs on the 29-bit-limb product (fr29.hpp; ~2x the
+// 8 x 32-bit product's rate): every trace value and constant enters in the
+// 29-bit form (x 2^261: a repack and a cheap reduction from the ark form),
+// sums and differences leave through the LDS-table reduction (< 2 r,
+// normalised), products stay as the multiplier leaves them (normalised,
+// < 8.92 r for inputs < 20 r), and the quotient value leaves canonical in the
+// ark form.  Bounds: add / sub inputs < 20 r give < 40 r with limbs < 1.5 2^30
+// (f29_reduce_qt takes < 64 r, limbs < 2.41 2^30); f29_sub16 takes a
+// subtrahend < 16 r.
+struct Q29 {
+    const uint4* qt;
+    __device__ __forceinline__ F29 add(const F29& a, const F29& b) const { return f29_reduce_qt(f29_lazy2(a, b), qt); }
+    __device__ __forceinline__ F29 sub(const F29& a, const F29& b) const { return f29_reduce_qt(f29_sub16(a, b), qt); }
+    __device__ __forceinline__ F29 mul(const F29& a, const F29& b) const { return f29_mul(a, b); }
+};
+
+__device__ __forceinline__ F29 ld29(const Fr* __restrict__ row, int32_t k) { return f29_from_fr(row[k]); }
+
+__device__ __forceinline__ F29 horner(const Q29& F, const Fr* __restrict__ row, const int32_t* __restrict__ ids,
+                                      int32_t n, const F29& a) {
+    F29 acc = f29_zero();
+    for (int32_t k = 0; k < n; ++k) acc = F.add(F.mul(acc, a), ld29(row, ids[k]));
     return acc;
 }
 
@@ -32,6 +51,10 @@ __global__ __launch_bounds__(256) void k_selector_denoms(const Fr* __restrict__ 
 }
 
 __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
+    f29_qtab_init(qt);
+    __syncthreads();
+    const Q29 F{qt};
     const size_t t = gtid();
     const size_t Q = 1ull << a.logQ;
     if (t >= (a.n ? a.n : Q)) return;  // n = Q >> log_step points
@@ -45,19 +68,20 @@ __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
     const size_t m = a.w >= 32 ? brev_bits(t, a.logQ - a.log_step) : t;
     const uint64_t i = a.i0 + ((uint64_t)m << a.log_step);
     const uint32_t qmask = (1u << a.log_q) - 1;
-    const Fr one = fr_one();
+    const F29 one = f29_from_fr(fr_one());
     const Fr x = fr_mul(a.gen, pow2l(a.tabQ, a.L1, i));
-    const Fr xm1 = fr_sub(x, one);
+    const Fr xm1 = fr_sub(x, fr_one());
     const Fr xml = fr_sub(x, a.wh_inv);
-    const Fr zh = a.zh[i & qmask];
-    const Fr first = fr_mul(zh, fr_mul(xml, a.inv_den[m]));  // Z_H / (x - 1)
-    const Fr last = fr_mul(zh, fr_mul(xm1, a.inv_den[m]));   // Z_H / (x - w^-1)
-    const Fr trans = xml;                                    // x - w^-1
+    const F29 zh = f29_from_fr(a.zh[i & qmask]), inv_den = f29_from_fr(a.inv_den[m]);
+    const F29 xml29 = f29_from_fr(xml);
+    const F29 first = F.mul(zh, F.mul(xml29, inv_den));              // Z_H / (x - 1)
+    const F29 last = F.mul(zh, F.mul(f29_from_fr(xm1), inv_den));  // Z_H / (x - w^-1)
+    const F29 trans = xml29;                                         // x - w^-1
     const Fr* loc = a.lde + (brev_bits(i, a.logQ) - a.row0) * a.w;
     const Fr* nxt = a.lde + (brev_bits((i + (1ull << a.log_q)) & (Q - 1), a.logQ) - a.row0) * a.w;
-    const Fr ap = a.pub_alpha, dl = a.pub_delta, al = a.alpha;
-    Fr acc = fr_zero();
-#define PUSH(X) acc = fr_add(fr_mul(acc, al), (X))
+    const F29 ap = f29_from_fr(a.pub_alpha), dl = f29_from_fr(a.pub_delta), al = f29_from_fr(a.alpha);
+    F29 acc = f29_zero();
+#define PUSH(X) acc = F.add(F.mul(acc, al), (X))
     const int32_t* d = a.air;
     int32_t p = 0;
     const int32_t ncfg = d[p++];
@@ -70,13 +94,14 @@ __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
             const int32_t* bid = d + p;
             p += nb;
             const int32_t binv = d[p++], chk = d[p++];
-            const Fr a_l = fr_add(horner(loc, aid, na, ap), dl);
-            const Fr b_l = fr_add(horner(loc, bid, nb, ap), dl);
-            PUSH(fr_sub(fr_mul(b_l, loc[binv]), one));
-            PUSH(fr_mul(first, fr_sub(loc[chk], fr_mul(a_l, loc[binv]))));
-            const Fr a_n = fr_add(horner(nxt, aid, na, ap), dl);
-            PUSH(fr_mul(trans, fr_sub(nxt[chk], fr_mul(fr_mul(loc[chk], a_n), nxt[binv]))));
-            PUSH(fr_mul(last, fr_sub(loc[chk], one)));
+            const F29 a_l = F.add(horner(F, loc, aid, na, ap), dl);
+            const F29 b_l = F.add(horner(F, loc, bid, nb, ap), dl);
+            const F29 lbinv = ld29(loc, binv), lchk = ld29(loc, chk);
+            PUSH(F.sub(F.mul(b_l, lbinv), one));
+            PUSH(F.mul(first, F.sub(lchk, F.mul(a_l, lbinv))));
+            const F29 a_n = F.add(horner(F, nxt, aid, na, ap), dl);
+            PUSH(F.mul(trans, F.sub(ld29(nxt, chk), F.mul(F.mul(lchk, a_n), ld29(nxt, binv)))));
+            PUSH(F.mul(last, F.sub(lchk, one)));
         } else {  // AirLookupConfig: air/src/lib.rs:57-114
             const int32_t na = d[p++];
             const int32_t* aid = d + p;
@@ -93,23 +118,26 @@ __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
             const int32_t* occ = d + p;
             p += nt;
             const int32_t chk = d[p++];
-            const Fr a_l = fr_add(horner(loc, aid, na, ap), dl);
-            PUSH(fr_sub(fr_mul(a_l, loc[ainv]), one));
-            Fr lc = fr_mul(loc[afil], loc[ainv]);
-            Fr nc = fr_mul(nxt[afil], nxt[ainv]);
+            const F29 a_l = F.add(horner(F, loc, aid, na, ap), dl);
+            const F29 lainv = ld29(loc, ainv);
+            PUSH(F.sub(F.mul(a_l, lainv), one));
+            F29 lc = F.mul(ld29(loc, afil), lainv);
+            F29 nc = F.mul(ld29(nxt, afil), ld29(nxt, ainv));
             for (int32_t t = 0; t < nt; ++t) {
-                const Fr b_l = fr_add(horner(loc, bid + t * nbc, nbc, ap), dl);
-                PUSH(fr_sub(fr_mul(b_l, loc[binv[t]]), one));
-                lc = fr_sub(lc, fr_mul(fr_mul(loc[bfil[t]], loc[occ[t]]), loc[binv[t]]));
-                nc = fr_sub(nc, fr_mul(fr_mul(nxt[bfil[t]], nxt[occ[t]]), nxt[binv[t]]));
+                const F29 b_l = F.add(horner(F, loc, bid + t * nbc, nbc, ap), dl);
+                const F29 lbinv = ld29(loc, binv[t]);
+                PUSH(F.sub(F.mul(b_l, lbinv), one));
+                lc = F.sub(lc, F.mul(F.mul(ld29(loc, bfil[t]), ld29(loc, occ[t])), lbinv));
+                nc = F.sub(nc, F.mul(F.mul(ld29(nxt, bfil[t]), ld29(nxt, occ[t])), ld29(nxt, binv[t])));
             }
-            PUSH(fr_mul(first, fr_sub(loc[chk], lc)));
-            PUSH(fr_mul(trans, fr_sub(fr_sub(nxt[chk], loc[chk]), nc)));
-            PUSH(fr_mul(last, loc[chk]));
+            const F29 lchk = ld29(loc, chk);
+            PUSH(F.mul(first, F.sub(lchk, lc)));
+            PUSH(F.mul(trans, F.sub(F.sub(ld29(nxt, chk), lchk), nc)));
+            PUSH(F.mul(last, lchk));
         }
     }
 #undef PUSH
-    a.out[m] = fr_mul(acc, a.inv_zh[i & qmask]);
+    a.out[m] = f29_to_fr_qt(F.mul(acc, f29_from_fr(a.inv_zh[i & qmask])), qt);
 }
 }  // namespace
 

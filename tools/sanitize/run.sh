@@ -30,7 +30,7 @@ for s in $SRCS; do
 done
 for p in "${pids[@]}"; do wait "$p"; done
 objs=$(for s in $SRCS; do echo -n "$OUT/${s%.*}.o "; done)
-$HIPCC -shared --offload-arch=gfx950 -fsanitize=address,undefined -shared-libsan -o "$OUT/liblsp_hip_asan.so" $objs -lpthread -ldl
+$HIPCC -shared --offload-arch=gfx950 -fno-gpu-sanitize -fsanitize=address,undefined -shared-libsan -o "$OUT/liblsp_hip_asan.so" $objs -lpthread -ldl
 # the driver is plain host C++ against include/lsp.h, built by the same clang
 CLANG=/opt/rocm/lib/llvm/bin/clang++
 RTDIR=$(dirname "$($CLANG -print-file-name=libclang_rt.asan-x86_64.so)")

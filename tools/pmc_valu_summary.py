@@ -6,7 +6,7 @@ GRBM_GUI_ACTIVE / 8 XCDs (MI355X_MICROARCH.md, DVFS note) -- the share of
 the chip's VALU issue slots the kernel used.  Also: effective clock,
 SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (share of wave time issuing VALU),
 LDS wait share and bank conflicts per LDS instruction."""
-import collections, csv, sys
+import collections, csv, os, sys
 
 root = sys.argv[1]
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -14,7 +14,10 @@ dur = collections.defaultdict(float)
 calls = collections.Counter()
 for p in ("p1", "p2", "p3"):
     seen = set()
-    for r in csv.DictReader(open(f"{root}/{p}/run_counter_collection.csv")):
+    path = f"{root}/{p}/run_counter_collection.csv"
+    if p != "p1" and not os.path.exists(path):  # tools/box_clock.sh runs no LDS pass
+        continue
+    for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"].replace("lsp::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         agg[name][r["Counter_Name"]] += float(r["Counter_Value"])
         key = (r["Dispatch_Id"], p)

@@ -78,6 +78,20 @@ typedef struct {
     uint32_t num_queries;          /* 33 (bin/src/main.rs:61) */
     uint32_t proof_of_work_bits;   /* 0  (bin/src/main.rs:62) */
     int32_t public_degree;         /* U6: symbolic degree of a public value, 1 (fork, default) or 0 */
+    /* U2/U3: the linear layers of Poseidon2Bls12337<3> (the fork's
+     * Poseidon2InternalLayer / Poseidon2ExternalLayer for WIDTH = 3, [EXT
+     * p3-bls12-377-fr]); NULL = the default, which is upstream Plonky3's
+     * width-3 template (p3-bn254-fr):
+     *   internal_diag  3 elements d: s_i <- (s0 + s1 + s2) + d_i s_i, i.e.
+     *                  M_I = J + diag(d); default d = (1, 1, 2)
+     *   external_mds   9 elements, row-major M_E: s <- M_E s before the first
+     *                  full round and after every full round; default
+     *                  circ(2, 1, 1), i.e. s_i += s0 + s1 + s2
+     * Montgomery form like round_constants.  Non-default layers cost 12
+     * products per full round and 3 per partial round more than the default
+     * (additions only) on every path: device, host scalar and host IFMA. */
+    const lsp_fr *internal_diag;
+    const lsp_fr *external_mds;
 } lsp_params;
 
 /* ---------------------------------------------------------------- library */

@@ -23,7 +23,8 @@ class LspParams(ctypes.Structure):
     _fields_ = [("sbox_degree", ctypes.c_uint32), ("rounds_f", ctypes.c_uint32), ("rounds_p", ctypes.c_uint32),
                 ("round_constants", ctypes.c_void_p), ("log_blowup", ctypes.c_uint32),
                 ("log_final_poly_len", ctypes.c_uint32), ("num_queries", ctypes.c_uint32),
-                ("proof_of_work_bits", ctypes.c_uint32), ("public_degree", ctypes.c_int32)]
+                ("proof_of_work_bits", ctypes.c_uint32), ("public_degree", ctypes.c_int32),
+                ("internal_diag", ctypes.c_void_p), ("external_mds", ctypes.c_void_p)]
 
 
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)

@@ -151,9 +151,37 @@ int lsp_ctx_create(int device, const lsp_params* p, lsp_ctx** out) {
         auto c = std::make_unique<lsp_ctx>();
         c->device = device;
         c->p2.L = P2Layout{p->rounds_f, p->rounds_p, p->sbox_degree};
-        const size_t nrc = 3 * p->rounds_f + p->rounds_p;
+        const size_t nround = 3 * p->rounds_f + p->rounds_p;
+        const size_t nrc = nround + P2_LIN_N;  // round constants, then M_E [9] and d [3]
         c->p2.rc.resize(nrc);
-        for (size_t i = 0; i < nrc; ++i) c->p2.rc[i] = to_fr(p->round_constants[i]);
+        for (size_t i = 0; i < nround; ++i) c->p2.rc[i] = to_fr(p->round_constants[i]);
+        {
+            // U2/U3: caller-set linear layers; the default values are stored
+            // too, and gen_lin picks the generic path only when they differ
+            static const uint32_t dm[9] = {2, 1, 1, 1, 2, 1, 1, 1, 2}, dd[3] = {1, 1, 2};
+            bool gen = false;
+            for (int k = 0; k < 9; ++k) {
+                const Fr def = fr_from_u64(dm[k]);
+                Fr v = def;
+                if (p->external_mds) {
+                    v = to_fr(p->external_mds[k]);
+                    LSP_REQUIRE(fr_words_lt_mod(v), LSP_E_ARG, "external_mds entry not canonical");
+                }
+                gen |= !fr_eq(v, def);
+                c->p2.rc[nround + k] = v;
+            }
+            for (int k = 0; k < 3; ++k) {
+                const Fr def = fr_from_u64(dd[k]);
+                Fr v = def;
+                if (p->internal_diag) {
+                    v = to_fr(p->internal_diag[k]);
+                    LSP_REQUIRE(fr_words_lt_mod(v), LSP_E_ARG, "internal_diag entry not canonical");
+                }
+                gen |= !fr_eq(v, def);
+                c->p2.rc[nround + 9 + k] = v;
+            }
+            c->p2.L.gen_lin = gen ? 1u : 0u;
+        }
         if (ifma::available()) ifma::prepare(c->p2.rc, c->p2.rc8);
         if (device != LSP_HOST_ONLY) {  // LSP_HOST_ONLY: verifier-only context, no GPU touched
             int n = 0;

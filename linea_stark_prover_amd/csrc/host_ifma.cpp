@@ -186,6 +186,7 @@ struct W {
 LSP_IFMA W mul(const W& a, const W& b) { return W{mul(a.x, b.x), mul(a.y, b.y)}; }
 LSP_IFMA W add(const W& a, const W& b) { return W{add(a.x, b.x), add(a.y, b.y)}; }
 LSP_IFMA W add(const W& a, const V& c) { return W{add(a.x, c), add(a.y, c)}; }
+LSP_IFMA W mul(const V& c, const W& a) { return W{mul(c, a.x), mul(c, a.y)}; }
 
 template <uint32_t D, class T>
 LSP_IFMA T sbox_t(const T& x) {
@@ -211,23 +212,49 @@ LSP_IFMA void ext_layer_t(T& s0, T& s1, T& s2) {
     s2 = add(s2, t);
 }
 
-// T = V (8 states) or W (16 states); round constants broadcast in V
+// caller-set U2/U3 layers (P2Layout::gen_lin; poseidon2_host64.hpp):
+// m = M_E row-major [9], d = the internal diagonal [3], broadcast in V
+template <class T>
+LSP_IFMA void ext_layer_gen_t(T& s0, T& s1, T& s2, const V* m) {
+    const T n0 = add(add(mul(m[0], s0), mul(m[1], s1)), mul(m[2], s2));
+    const T n1 = add(add(mul(m[3], s0), mul(m[4], s1)), mul(m[5], s2));
+    const T n2 = add(add(mul(m[6], s0), mul(m[7], s1)), mul(m[8], s2));
+    s0 = n0;
+    s1 = n1;
+    s2 = n2;
+}
+
+// T = V (8 states) or W (16 states); round constants broadcast in V; lin:
+// nullptr = the default U2/U3 layers, else M_E [9] then d [3]
 template <uint32_t D, class T>
-LSP_IFMA void permute(T& s0, T& s1, T& s2, const V* rc, uint32_t rounds_f, uint32_t rounds_p) {
+LSP_IFMA void permute(T& s0, T& s1, T& s2, const V* rc, uint32_t rounds_f, uint32_t rounds_p,
+                      const V* lin = nullptr) {
     const uint32_t half = rounds_f / 2;
     const V* ini = rc;
     const V* ter = rc + 3 * half;
     const V* itl = rc + 6 * half;
-    ext_layer_t(s0, s1, s2);
+    if (lin)
+        ext_layer_gen_t(s0, s1, s2, lin);
+    else
+        ext_layer_t(s0, s1, s2);
     for (uint32_t r = 0; r < half; ++r) {
         s0 = sbox_t<D>(add(s0, ini[3 * r + 0]));
         s1 = sbox_t<D>(add(s1, ini[3 * r + 1]));
         s2 = sbox_t<D>(add(s2, ini[3 * r + 2]));
-        ext_layer_t(s0, s1, s2);
+        if (lin)
+            ext_layer_gen_t(s0, s1, s2, lin);
+        else
+            ext_layer_t(s0, s1, s2);
     }
     for (uint32_t r = 0; r < rounds_p; ++r) {
         s0 = sbox_t<D>(add(s0, itl[r]));
         const T t = add(add(s0, s1), s2);
+        if (lin) {
+            s0 = add(t, mul(lin[9], s0));
+            s1 = add(t, mul(lin[10], s1));
+            s2 = add(t, mul(lin[11], s2));
+            continue;
+        }
         s0 = add(s0, t);
         s1 = add(s1, t);
         s2 = add(add(s2, s2), t);
@@ -236,7 +263,10 @@ LSP_IFMA void permute(T& s0, T& s1, T& s2, const V* rc, uint32_t rounds_f, uint3
         s0 = sbox_t<D>(add(s0, ter[3 * r + 0]));
         s1 = sbox_t<D>(add(s1, ter[3 * r + 1]));
         s2 = sbox_t<D>(add(s2, ter[3 * r + 2]));
-        ext_layer_t(s0, s1, s2);
+        if (lin)
+            ext_layer_gen_t(s0, s1, s2, lin);
+        else
+            ext_layer_t(s0, s1, s2);
     }
 }
 
@@ -249,12 +279,15 @@ __attribute__((target("avx512f,avx512ifma"))) void rc_to_ifma(const Fr* rc, size
     }
 }
 
+// the generic layers' constants, after the round constants (poseidon2.hpp)
+inline const V* lin_ptr(const V* rc, const P2Layout& L) { return L.gen_lin ? rc + p2_lin_offset(L) : nullptr; }
+
 template <uint32_t D>
 __attribute__((target("avx512f,avx512ifma"))) void compress8_t(const Fr* left, const Fr* right, size_t stride,
                                                                 Fr* out, int n, const V* rc, const P2Layout& L) {
     V s0 = load(left, stride, n), s1 = load(right, stride, n), s2;
     for (int k = 0; k < 5; ++k) s2.l[k] = _mm512_setzero_si512();
-    permute<D>(s0, s1, s2, rc, L.rounds_f, L.rounds_p);
+    permute<D>(s0, s1, s2, rc, L.rounds_f, L.rounds_p, lin_ptr(rc, L));
     store(s0, out, 1, n);
 }
 
@@ -266,7 +299,7 @@ __attribute__((target("avx512f,avx512ifma"))) void compress16_t(const Fr* left, 
     W s1{load(right, stride, n1), load(right + 8 * stride, stride, n2)};
     W s2;
     for (int k = 0; k < 5; ++k) s2.x.l[k] = s2.y.l[k] = _mm512_setzero_si512();
-    permute<D>(s0, s1, s2, rc, L.rounds_f, L.rounds_p);
+    permute<D>(s0, s1, s2, rc, L.rounds_f, L.rounds_p, lin_ptr(rc, L));
     store(s0.x, out, 1, n1);
     store(s0.y, out + 8, 1, n2);
 }
@@ -280,12 +313,12 @@ __attribute__((target("avx512f,avx512ifma"))) void hash8_t(const Fr* rows, size_
     while (k + 2 <= w) {
         s0 = load(rows + k, w, n);
         s1 = load(rows + k + 1, w, n);
-        permute<D>(s0, s1, s2, rc, L.rounds_f, L.rounds_p);
+        permute<D>(s0, s1, s2, rc, L.rounds_f, L.rounds_p, lin_ptr(rc, L));
         k += 2;
     }
     if (k < w) {
         s0 = load(rows + k, w, n);
-        permute<D>(s0, s1, s2, rc, L.rounds_f, L.rounds_p);
+        permute<D>(s0, s1, s2, rc, L.rounds_f, L.rounds_p, lin_ptr(rc, L));
     }
     store(s0, out, 1, n);
 }

@@ -33,7 +33,7 @@ __global__ __launch_bounds__(256) void k_permute(Fr* __restrict__ st, size_t n, 
     const size_t i = gtid();
     if (i >= n) return;
     F29 s0 = f29_from_fr(st[3 * i]), s1 = f29_from_fr(st[3 * i + 1]), s2 = f29_from_fr(st[3 * i + 2]);
-    permute3_f29<D>(s0, s1, s2, rc, rf, rp, qt);
+    permute3_any<D, 1>(s0, s1, s2, rc, rf, rp, qt);
     st[3 * i] = f29_to_fr(s0);
     st[3 * i + 1] = f29_to_fr(s1);
     st[3 * i + 2] = f29_to_fr(s2);
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void k_grind(Fr pre0, Fr pre1, Fr pre2, uint32
         const uint64_t w = base + i;
         const F29 fw = f29_from_fr(fr_from_u64(w));
         F29 s0 = wlane == 0 ? fw : c0, s1 = wlane == 0 ? c1 : fw, s2 = c2;
-        permute3_f29<D>(s0, s1, s2, rc, rf, rp, qt);
+        permute3_any<D, 1>(s0, s1, s2, rc, rf, rp, qt);
         const Fr c = fr_to_canonical(f29_to_fr(s0));
         const uint64_t lo = (uint64_t)c.v[0] | ((uint64_t)c.v[1] << 32);
         if ((lo & mask) == 0) atomicMin(best, (unsigned long long)w);
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void k_calib_perm(Fr* __restrict__ out, uint32
     __syncthreads();
     const size_t t = gtid();
     F29 s0 = f29_from_fr(fr_from_u64(t + 1)), s1 = f29_from_fr(fr_from_u64(3 * t + 7)), s2 = f29_zero();
-    for (uint32_t i = 0; i < iters; ++i) permute3_f29<D>(s0, s1, s2, rc, rf, rp, qt);
+    for (uint32_t i = 0; i < iters; ++i) permute3_any<D, 1>(s0, s1, s2, rc, rf, rp, qt);
     out[t] = f29_to_fr(s0);
 }
 
@@ -192,9 +192,15 @@ hipError_t launch_rc_to_f29(const Fr* rc, F29* rc29, uint32_t n, hipStream_t st)
     return hipGetLastError();
 }
 
+// D = the S-box degree, | P2_GEN for caller-set linear layers (gen_lin)
 #define LSP_DISPATCH_D(L, KERNEL, ...)                                  \
     do {                                                                \
-        if ((L).sbox_degree == 17)                                      \
+        if ((L).gen_lin) {                                              \
+            if ((L).sbox_degree == 17)                                  \
+                hipLaunchKernelGGL(KERNEL<17u | P2_GEN>, __VA_ARGS__);  \
+            else                                                        \
+                hipLaunchKernelGGL(KERNEL<11u | P2_GEN>, __VA_ARGS__);  \
+        } else if ((L).sbox_degree == 17)                               \
             hipLaunchKernelGGL(KERNEL<17>, __VA_ARGS__);                \
         else                                                            \
             hipLaunchKernelGGL(KERNEL<11>, __VA_ARGS__);                \
@@ -204,23 +210,26 @@ hipError_t launch_rc_to_f29(const Fr* rc, F29* rc29, uint32_t n, hipStream_t st)
 // state per DPP quad: 4 * COOP_MAX lanes = one wave per SIMD of the 256 CUs,
 // where the quad form's shorter critical path (30 vs 46 S-boxes) wins; wider
 // batches are throughput-bound and keep one state per lane.
+#define LSP_DISPATCH_DL(DEG, LANES, KERNEL, ...)                          \
+    do {                                                                  \
+        if ((LANES) == 4)                                                 \
+            hipLaunchKernelGGL((KERNEL<DEG, 4>), __VA_ARGS__);            \
+        else if ((LANES) == 2)                                            \
+            hipLaunchKernelGGL((KERNEL<DEG, 2>), __VA_ARGS__);            \
+        else                                                              \
+            hipLaunchKernelGGL((KERNEL<DEG, 1>), __VA_ARGS__);            \
+    } while (0)
 #define LSP_DISPATCH_DC(L, LANES, KERNEL, ...)                            \
     do {                                                                  \
-        if ((L).sbox_degree == 17) {                                      \
-            if ((LANES) == 4)                                             \
-                hipLaunchKernelGGL((KERNEL<17, 4>), __VA_ARGS__);         \
-            else if ((LANES) == 2)                                        \
-                hipLaunchKernelGGL((KERNEL<17, 2>), __VA_ARGS__);         \
+        if ((L).gen_lin) {                                                \
+            if ((L).sbox_degree == 17)                                    \
+                LSP_DISPATCH_DL(17u | P2_GEN, LANES, KERNEL, __VA_ARGS__);\
             else                                                          \
-                hipLaunchKernelGGL((KERNEL<17, 1>), __VA_ARGS__);         \
-        } else {                                                          \
-            if ((LANES) == 4)                                             \
-                hipLaunchKernelGGL((KERNEL<11, 4>), __VA_ARGS__);         \
-            else if ((LANES) == 2)                                        \
-                hipLaunchKernelGGL((KERNEL<11, 2>), __VA_ARGS__);         \
-            else                                                          \
-                hipLaunchKernelGGL((KERNEL<11, 1>), __VA_ARGS__);         \
-        }                                                                 \
+                LSP_DISPATCH_DL(11u | P2_GEN, LANES, KERNEL, __VA_ARGS__);\
+        } else if ((L).sbox_degree == 17)                                 \
+            LSP_DISPATCH_DL(17u, LANES, KERNEL, __VA_ARGS__);             \
+        else                                                              \
+            LSP_DISPATCH_DL(11u, LANES, KERNEL, __VA_ARGS__);             \
     } while (0)
 
 static size_t coop_max() {

@@ -8,15 +8,25 @@
 // (diag (1,1,2)); U3 external layer circ(2,1,1) = s_i += sum, applied once
 // before the first full round.  Round constants (U4) are supplied by the
 // caller in new_from_rng order: initial external [rf/2][3], terminal external
-// [rf/2][3], internal [rp].
+// [rf/2][3], internal [rp].  The 8 x 32-bit permute3 below has the default
+// U2/U3 layers only (micro-benchmarks); the product's permutations
+// (poseidon2_f29.hpp, poseidon2_host64.hpp, host_ifma.cpp) also take
+// caller-set layers (P2Layout::gen_lin).
 #pragma once
 #include "fr.hpp"
 
 namespace lsp {
 
+// gen_lin: non-default U2/U3 linear layers (lsp_params.internal_diag /
+// external_mds).  Their constants follow the round constants in every
+// constant array (host Fr, device F29, IFMA lanes): M_E row-major [9], then
+// the internal diagonal d [3] (p2_lin_offset).
 struct P2Layout {
     uint32_t rounds_f, rounds_p, sbox_degree;
+    uint32_t gen_lin = 0;
 };
+constexpr uint32_t P2_LIN_N = 12;
+LSP_HD uint32_t p2_lin_offset(const P2Layout& L) { return 3 * L.rounds_f + L.rounds_p; }
 
 LSP_HD Fr sbox(const Fr& x, uint32_t d) {
     Fr x2 = fr_sqr(x);
@@ -68,13 +78,6 @@ LSP_HD void permute3(Fr& s0, Fr& s1, Fr& s2, const Fr* __restrict__ rc, uint32_t
         s2 = sbox(fr_add(s2, ter[3 * r + 2]), D);
         ext_layer(s0, s1, s2);
     }
-}
-
-LSP_HD void permute3_rt(Fr& s0, Fr& s1, Fr& s2, const Fr* rc, const P2Layout& L) {
-    if (L.sbox_degree == 17)
-        permute3<17>(s0, s1, s2, rc, L.rounds_f, L.rounds_p);
-    else
-        permute3<11>(s0, s1, s2, rc, L.rounds_f, L.rounds_p);
 }
 
 // PaddingFreeSponge<Perm,3,2,1>::hash_iter over n elements read by `get(k)`:

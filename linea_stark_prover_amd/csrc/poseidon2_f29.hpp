@@ -235,11 +235,106 @@ __device__ __forceinline__ void permute3_f29_coop(F29& s0, F29& s1, F29& s2, con
     s2 = f29_add(s2, t);
 }
 
-// LANES: lanes per state (1, 2: pair_, 4: quad-cooperative)
+// ---- caller-set U2/U3 linear layers (lsp_params.internal_diag /
+// external_mds; P2Layout::gen_lin).  The default layers above are additions
+// folded lazily into the S-box inputs; a general M_E and M_I = J + diag(d)
+// need products, so this variant keeps every state value normalised and
+// < 2 r between layers (f29_reduce after each sum) and pays 9 products per
+// external layer and 3 per internal layer.  Bounds: S-box inputs s + c < 4 r,
+// outputs < 8.2 r; a layer's products (constants < 2 r) < 8.2 r, sums of
+// three < 25 r < 2^261.  The constants follow the round constants in rc29:
+// M_E row-major [9], then d [3] (poseidon2.hpp).  Kernels select it with the
+// template flag P2_GEN on D.
+constexpr uint32_t P2_GEN = 0x100u;
+
+__device__ __forceinline__ void ext_layer_gen29(F29& s0, F29& s1, F29& s2, const F29* __restrict__ m) {
+    F29 n[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        n[i] = f29_reduce(f29_add(f29_lazy2(f29_mul(m[3 * i], s0), f29_mul(m[3 * i + 1], s1)), f29_mul(m[3 * i + 2], s2)));
+    s0 = n[0];
+    s1 = n[1];
+    s2 = n[2];
+}
+
+__device__ __forceinline__ void int_layer_gen29(F29& s0, F29& s1, F29& s2, const F29* __restrict__ d) {
+    const F29 u = f29_lazy3(s0, s1, s2);  // < 12.2 r, limbs < 3 2^29
+    s0 = f29_reduce(f29_add(u, f29_mul(d[0], s0)));
+    s1 = f29_reduce(f29_add(u, f29_mul(d[1], s1)));
+    s2 = f29_reduce(f29_add(u, f29_mul(d[2], s2)));
+}
+
+// the three S-boxes of a full round on 1, 2 (pair) or 4 (quad) lanes per state
+template <uint32_t D, int LANES>
+__device__ __forceinline__ void full_sboxes_gen29(F29& s0, F29& s1, F29& s2) {
+    if constexpr (LANES == 1) {
+        s0 = sbox29<D>(s0);
+        s1 = sbox29<D>(s1);
+        s2 = sbox29<D>(s2);
+    } else if constexpr (LANES == 2) {
+        const uint32_t m1 = 0u - (threadIdx.x & 1u);
+        F29 in;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) in.l[i] = (s0.l[i] & ~m1) | (s1.l[i] & m1);
+        const F29 xa = sbox29<D>(in);
+        s2 = sbox29<D>(s2);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            s0.l[i] = pair_bcast(xa.l[i], 0);
+            s1.l[i] = pair_bcast(xa.l[i], 1);
+        }
+    } else {
+        const F29 x = sbox29<D>(f29_sel3(min(threadIdx.x & 3u, 2u), s0, s1, s2));
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            s0.l[i] = quad_bcast(x.l[i], 0);
+            s1.l[i] = quad_bcast(x.l[i], 1);
+            s2.l[i] = quad_bcast(x.l[i], 2);
+        }
+    }
+}
+
+template <uint32_t D, int LANES>
+__device__ __forceinline__ void permute3_f29_gen(F29& s0, F29& s1, F29& s2, const F29* __restrict__ rc29,
+                                                 uint32_t rf, uint32_t rp) {
+    const uint32_t half = rf / 2;
+    const F29* ini = rc29;
+    const F29* ter = rc29 + 3 * half;
+    const F29* itl = rc29 + 6 * half;
+    const F29* lin = rc29 + 3 * rf + rp;
+    ext_layer_gen29(s0, s1, s2, lin);
+    for (uint32_t r = 0; r < half; ++r) {
+        s0 = f29_add(s0, ini[3 * r + 0]);
+        s1 = f29_add(s1, ini[3 * r + 1]);
+        s2 = f29_add(s2, ini[3 * r + 2]);
+        full_sboxes_gen29<D, LANES>(s0, s1, s2);
+        ext_layer_gen29(s0, s1, s2, lin);
+    }
+    for (uint32_t r = 0; r < rp; ++r) {
+        const F29 x = f29_add(s0, itl[r]);
+        if constexpr (LANES == 1)
+            s0 = sbox29<D>(x);
+        else
+            s0 = sbox29_coop<D, LANES>(x);
+        int_layer_gen29(s0, s1, s2, lin + 9);
+    }
+    for (uint32_t r = 0; r < half; ++r) {
+        s0 = f29_add(s0, ter[3 * r + 0]);
+        s1 = f29_add(s1, ter[3 * r + 1]);
+        s2 = f29_add(s2, ter[3 * r + 2]);
+        full_sboxes_gen29<D, LANES>(s0, s1, s2);
+        ext_layer_gen29(s0, s1, s2, lin);
+    }
+}
+
+// LANES: lanes per state (1, 2: pair_, 4: quad-cooperative); D: the S-box
+// degree, with P2_GEN set for caller-set linear layers
 template <uint32_t D, int LANES = 1>
 __device__ __forceinline__ void permute3_any(F29& s0, F29& s1, F29& s2, const F29* __restrict__ rc29, uint32_t rf,
                                              uint32_t rp, const uint4* __restrict__ qt) {
-    if (LANES == 4)
+    if constexpr ((D & P2_GEN) != 0)
+        permute3_f29_gen<(D & ~P2_GEN), LANES>(s0, s1, s2, rc29, rf, rp);
+    else if (LANES == 4)
         permute3_f29_coop<D>(s0, s1, s2, rc29, rf, rp, qt);
     else if (LANES == 2)
         permute3_f29_pair<D>(s0, s1, s2, rc29, rf, rp, qt);

@@ -254,23 +254,53 @@ inline void ext_layer(F& s0, F& s1, F& s2) {
     s2 = add(s2, t);
 }
 
-// rc: constants in new_from_rng order (poseidon2.hpp); states in and out canonical
+// caller-set U2/U3 layers (P2Layout::gen_lin): s <- M_E s and
+// s_i <- (s0 + s1 + s2) + d_i s_i, products of values < 2r (< 1.3 r)
+inline void ext_layer_gen(F& s0, F& s1, F& s2, const Fr* m) {
+    F n[3];
+    for (int i = 0; i < 3; ++i)
+        n[i] = add(add(mul(from(m[3 * i]), s0), mul(from(m[3 * i + 1]), s1)), mul(from(m[3 * i + 2]), s2));
+    s0 = n[0];
+    s1 = n[1];
+    s2 = n[2];
+}
+
+inline void int_layer_gen(F& s0, F& s1, F& s2, const Fr* d) {
+    const F t = add(add(s0, s1), s2);
+    s0 = add(t, mul(from(d[0]), s0));
+    s1 = add(t, mul(from(d[1]), s1));
+    s2 = add(t, mul(from(d[2]), s2));
+}
+
+// rc: constants in new_from_rng order (poseidon2.hpp); states in and out
+// canonical.  lin: nullptr = the default U2/U3 layers, else M_E [9] then d [3]
 template <uint32_t D>
-inline void permute3(Fr& a0, Fr& a1, Fr& a2, const Fr* rc, uint32_t rounds_f, uint32_t rounds_p) {
+inline void permute3(Fr& a0, Fr& a1, Fr& a2, const Fr* rc, uint32_t rounds_f, uint32_t rounds_p,
+                     const Fr* lin = nullptr) {
     const uint32_t half = rounds_f / 2;
     const Fr* ini = rc;
     const Fr* ter = rc + 3 * half;
     const Fr* itl = rc + 6 * half;
     F s0 = from(a0), s1 = from(a1), s2 = from(a2);
-    ext_layer(s0, s1, s2);
+    auto ext = [&] {
+        if (lin)
+            ext_layer_gen(s0, s1, s2, lin);
+        else
+            ext_layer(s0, s1, s2);
+    };
+    ext();
     for (uint32_t r = 0; r < half; ++r) {
         s0 = sbox<D>(add(s0, from(ini[3 * r + 0])));
         s1 = sbox<D>(add(s1, from(ini[3 * r + 1])));
         s2 = sbox<D>(add(s2, from(ini[3 * r + 2])));
-        ext_layer(s0, s1, s2);
+        ext();
     }
     for (uint32_t r = 0; r < rounds_p; ++r) {
         s0 = sbox<D>(add(s0, from(itl[r])));
+        if (lin) {
+            int_layer_gen(s0, s1, s2, lin + 9);
+            continue;
+        }
         const F t = add(add(s0, s1), s2);
         s0 = add(s0, t);
         s1 = add(s1, t);
@@ -280,7 +310,7 @@ inline void permute3(Fr& a0, Fr& a1, Fr& a2, const Fr* rc, uint32_t rounds_f, ui
         s0 = sbox<D>(add(s0, from(ter[3 * r + 0])));
         s1 = sbox<D>(add(s1, from(ter[3 * r + 1])));
         s2 = sbox<D>(add(s2, from(ter[3 * r + 2])));
-        ext_layer(s0, s1, s2);
+        ext();
     }
     a0 = to_canonical(s0);
     a1 = to_canonical(s1);
@@ -288,10 +318,11 @@ inline void permute3(Fr& a0, Fr& a1, Fr& a2, const Fr* rc, uint32_t rounds_f, ui
 }
 
 inline void permute3_rt(Fr& s0, Fr& s1, Fr& s2, const Fr* rc, const P2Layout& L) {
+    const Fr* lin = L.gen_lin ? rc + p2_lin_offset(L) : nullptr;
     if (L.sbox_degree == 17)
-        permute3<17>(s0, s1, s2, rc, L.rounds_f, L.rounds_p);
+        permute3<17>(s0, s1, s2, rc, L.rounds_f, L.rounds_p, lin);
     else
-        permute3<11>(s0, s1, s2, rc, L.rounds_f, L.rounds_p);
+        permute3<11>(s0, s1, s2, rc, L.rounds_f, L.rounds_p, lin);
 }
 
 }  // namespace hp64

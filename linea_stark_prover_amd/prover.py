@@ -52,6 +52,10 @@ class StarkConfig:
     proof_of_work_bits: int = 0
     public_degree: int = 1          # U6
     seed: int = DEFAULT_SEED        # U4/U5
+    # U2/U3, the Poseidon2 linear layers (include/lsp.h): canonical ints,
+    # None = the default layer (internal diag (1, 1, 2); external circ(2, 1, 1))
+    internal_diag: Optional[Tuple[int, int, int]] = None
+    external_mds: Optional[Tuple[int, ...]] = None   # 9 entries, row-major
 
     def seeded(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """(alpha, delta, round_constants) from the documented seeded generator."""
@@ -83,9 +87,14 @@ class Context:
         if round_constants is None:
             _, _, round_constants = config.seeded()
         self._rc = _fr_arr(round_constants)
+        self._diag = None if config.internal_diag is None else to_mont(config.internal_diag)
+        self._mds = None if config.external_mds is None else to_mont(config.external_mds)
+        assert self._diag is None or self._diag.shape[0] == 3, "internal_diag needs 3 entries"
+        assert self._mds is None or self._mds.shape[0] == 9, "external_mds needs 9 entries"
         p = L.LspParams(config.sbox_degree, config.rounds_f, config.rounds_p, _ptr(self._rc), config.log_blowup,
                         config.log_final_poly_len, config.num_queries, config.proof_of_work_bits,
-                        config.public_degree)
+                        config.public_degree, None if self._diag is None else _ptr(self._diag),
+                        None if self._mds is None else _ptr(self._mds))
         h = ctypes.c_void_p()
         L.check(L.lib().lsp_ctx_create(device, ctypes.byref(p), ctypes.byref(h)))
         self.h = h

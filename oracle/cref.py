@@ -22,7 +22,9 @@ class Params(ctypes.Structure):
                 ("ext_initial", ctypes.c_uint64 * (8 * 3 * 4)),
                 ("ext_terminal", ctypes.c_uint64 * (8 * 3 * 4)),
                 ("internal", ctypes.c_uint64 * (64 * 4)),
-                ("alpha", ctypes.c_uint64 * 4), ("delta", ctypes.c_uint64 * 4)]
+                ("alpha", ctypes.c_uint64 * 4), ("delta", ctypes.c_uint64 * 4),
+                ("generic_lin", ctypes.c_uint32),
+                ("ext_mds", ctypes.c_uint64 * (9 * 4)), ("int_diag", ctypes.c_uint64 * (3 * 4))]
 
 
 class Fri(ctypes.Structure):
@@ -102,13 +104,38 @@ def params_from_setup(s: O.Setup) -> Params:
         put(p.internal, r, rc)
     put(p.alpha, 0, s.alpha)
     put(p.delta, 0, s.delta)
+    set_linear_layers(p, s.perm.int_diag, s.perm.ext_mds)
     return p
 
 
-def setup(seed: int = O.DEFAULT_SEED, sbox_degree=11, rounds_f=8, rounds_p=22) -> Params:
+def _put(arr, idx, v):
+    raw = O.to_mont_bytes(v)
+    for k in range(4):
+        arr[idx * 4 + k] = int.from_bytes(raw[8 * k:8 * k + 8], "little")
+
+
+def set_linear_layers(p: Params, int_diag=None, ext_mds=None) -> Params:
+    """U2/U3: internal diag d (3 ints) and external M_E (9 ints, row-major);
+    None = the default layer.  Both None -> generic_lin = 0 (default path)."""
+    if int_diag is None and ext_mds is None:
+        p.generic_lin = 0
+        return p
+    d = O.DEFAULT_INT_DIAG if int_diag is None else int_diag
+    m = O.DEFAULT_EXT_MDS if ext_mds is None else ext_mds
+    assert len(d) == 3 and len(m) == 9
+    for i, v in enumerate(m):
+        _put(p.ext_mds, i, v % O.P)
+    for i, v in enumerate(d):
+        _put(p.int_diag, i, v % O.P)
+    p.generic_lin = 1
+    return p
+
+
+def setup(seed: int = O.DEFAULT_SEED, sbox_degree=11, rounds_f=8, rounds_p=22, int_diag=None,
+          ext_mds=None) -> Params:
     p = Params()
     lib().lo_setup(ctypes.c_uint64(seed), sbox_degree, rounds_f, rounds_p, ctypes.byref(p))
-    return p
+    return set_linear_layers(p, int_diag, ext_mds)
 
 
 def fri_params(fp: O.FriParams = O.FriParams()) -> Fri:

@@ -325,6 +325,28 @@ static inline void sbox(const lo_params *p, lo_fr *x) {
     fpow64(x, p->sbox_degree, &r);
     *x = r;
 }
+/* generic U2/U3 layers (lo_params.generic_lin) */
+static void ext_layer_gen(const lo_params *p, lo_fr s[3]) {
+    lo_fr o[3];
+    for (int i = 0; i < 3; ++i) {
+        lo_fr acc = ZERO_FR, t;
+        for (int j = 0; j < 3; ++j) {
+            fmul(&p->ext_mds[3 * i + j], &s[j], &t);
+            fadd(&acc, &t, &acc);
+        }
+        o[i] = acc;
+    }
+    for (int i = 0; i < 3; ++i) s[i] = o[i];
+}
+static void int_layer_gen(const lo_params *p, lo_fr s[3]) {
+    lo_fr u, t;
+    fadd(&s[0], &s[1], &u);
+    fadd(&u, &s[2], &u);
+    for (int i = 0; i < 3; ++i) {
+        fmul(&p->int_diag[i], &s[i], &t);
+        fadd(&u, &t, &s[i]);
+    }
+}
 static inline void ext_layer(lo_fr s[3]) {
     lo_fr t;
     fadd(&s[0], &s[1], &t);
@@ -344,26 +366,32 @@ static inline void int_layer(lo_fr s[3]) {
 }
 void lo_poseidon2_permute(const lo_params *p, lo_fr s[3]) {
     field_init();
-    ext_layer(s);
+    const int gen = p->generic_lin != 0;
+#define EXT() (gen ? ext_layer_gen(p, s) : ext_layer(s))
+    EXT();
     for (uint32_t r = 0; r < p->rounds_f / 2; ++r) {
         for (int i = 0; i < 3; ++i) {
             fadd(&s[i], &p->ext_initial[r][i], &s[i]);
             sbox(p, &s[i]);
         }
-        ext_layer(s);
+        EXT();
     }
     for (uint32_t r = 0; r < p->rounds_p; ++r) {
         fadd(&s[0], &p->internal[r], &s[0]);
         sbox(p, &s[0]);
-        int_layer(s);
+        if (gen)
+            int_layer_gen(p, s);
+        else
+            int_layer(s);
     }
     for (uint32_t r = 0; r < p->rounds_f / 2; ++r) {
         for (int i = 0; i < 3; ++i) {
             fadd(&s[i], &p->ext_terminal[r][i], &s[i]);
             sbox(p, &s[i]);
         }
-        ext_layer(s);
+        EXT();
     }
+#undef EXT
 }
 
 /* PaddingFreeSponge<Perm,3,2,1>: overwrite-mode, no padding */

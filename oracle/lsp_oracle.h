@@ -31,6 +31,12 @@ typedef struct {
     lo_fr ext_terminal[8][3];
     lo_fr internal[64];
     lo_fr alpha, delta; /* permutation challenges (public values) */
+    /* U2/U3 linear layers: generic_lin == 0 -> the defaults (external
+     * circ(2,1,1), internal J + diag(1,1,2)); otherwise s <- ext_mds s
+     * (row-major) and s_i <- (s0+s1+s2) + int_diag[i] s_i */
+    uint32_t generic_lin;
+    lo_fr ext_mds[9];
+    lo_fr int_diag[3];
 } lo_params;
 
 typedef struct {

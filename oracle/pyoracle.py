@@ -30,7 +30,7 @@ from __future__ import annotations
 
 import struct
 from dataclasses import dataclass, field
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 # ---------------------------------------------------------------------------
 # A1 -- BLS12-377 scalar field Fr (ark-bls12-377 0.5.0, Cargo.lock:51;
@@ -140,9 +140,17 @@ class SplitMix64:
 
 # ---------------------------------------------------------------------------
 # A3 -- Poseidon2Bls12337<3> (bin/src/config.rs:11), Perm::new_from_rng(8, 22)
-# (bin/src/main.rs:49).  U1: S-box x^11.  U2: internal diag (1,1,2).
-# U3: external circ(2,1,1), applied once before the first full round.
+# (bin/src/main.rs:49).  U1: S-box x^11.  U2: internal layer M_I = J + diag(d),
+# s_i <- (s0 + s1 + s2) + d_i s_i, default d = (1, 1, 2) (the Bn254 template of
+# upstream Plonky3's width-3 internal layer).  U3: external layer M_E, applied
+# once before the first full round and after every full round, default
+# circ(2, 1, 1) (s_i += s0 + s1 + s2).  Both are parameters (int_diag,
+# ext_mds; None = default) so a caller whose fork uses other layers can set them.
 # ---------------------------------------------------------------------------
+DEFAULT_INT_DIAG = (1, 1, 2)
+DEFAULT_EXT_MDS = (2, 1, 1, 1, 2, 1, 1, 1, 2)
+
+
 @dataclass
 class Poseidon2Params:
     sbox_degree: int = 11
@@ -151,6 +159,8 @@ class Poseidon2Params:
     ext_initial: List[List[int]] = field(default_factory=list)   # rounds_f/2 x 3
     ext_terminal: List[List[int]] = field(default_factory=list)  # rounds_f/2 x 3
     internal: List[int] = field(default_factory=list)            # rounds_p
+    int_diag: Optional[Sequence[int]] = None   # U2: d (3 ints mod P); None = (1, 1, 2)
+    ext_mds: Optional[Sequence[int]] = None    # U3: M_E row-major (9 ints mod P); None = circ(2, 1, 1)
 
 
 @dataclass
@@ -175,28 +185,34 @@ def setup_from_seed(seed: int = DEFAULT_SEED, sbox_degree: int = 11,
     return Setup(alpha, delta, Poseidon2Params(sbox_degree, rounds_f, rounds_p, ini, ter, internal))
 
 
-def _ext_layer(s):
-    t = (s[0] + s[1] + s[2]) % P
-    return [(s[0] + t) % P, (s[1] + t) % P, (s[2] + t) % P]
+def _ext_layer(s, m=None):
+    """s <- M_E s; M_E = circ(2, 1, 1) (s_i += s0 + s1 + s2) unless given."""
+    if m is None:
+        t = (s[0] + s[1] + s[2]) % P
+        return [(s[0] + t) % P, (s[1] + t) % P, (s[2] + t) % P]
+    return [(m[3 * i] * s[0] + m[3 * i + 1] * s[1] + m[3 * i + 2] * s[2]) % P for i in range(3)]
 
 
-def _int_layer(s):
+def _int_layer(s, d=None):
+    """s_i <- (s0 + s1 + s2) + d_i s_i; d = (1, 1, 2) unless given."""
+    d = DEFAULT_INT_DIAG if d is None else d
     t = (s[0] + s[1] + s[2]) % P
-    return [(s[0] + t) % P, (s[1] + t) % P, (2 * s[2] + t) % P]
+    return [(t + d[i] * s[i]) % P for i in range(3)]
 
 
 def permute(state: Sequence[int], pp: Poseidon2Params) -> List[int]:
     d = pp.sbox_degree
-    s = _ext_layer(list(state))
+    m, dg = pp.ext_mds, pp.int_diag
+    s = _ext_layer(list(state), m)
     for rc in pp.ext_initial:
         s = [pow((s[i] + rc[i]) % P, d, P) for i in range(3)]
-        s = _ext_layer(s)
+        s = _ext_layer(s, m)
     for rc in pp.internal:
         s[0] = pow((s[0] + rc) % P, d, P)
-        s = _int_layer(s)
+        s = _int_layer(s, dg)
     for rc in pp.ext_terminal:
         s = [pow((s[i] + rc[i]) % P, d, P) for i in range(3)]
-        s = _ext_layer(s)
+        s = _ext_layer(s, m)
     return s
 
 

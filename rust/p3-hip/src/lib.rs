@@ -26,7 +26,7 @@ mod proof;
 pub use dft::HipDft;
 pub use fri::HipFriFolder;
 pub use mmcs::{HipMmcs, HipMmcsError, HipTree};
-pub use proof::{from_proof, prove, proof_from_bytes, proof_to_bytes, to_proof};
+pub use proof::{from_proof, prove, proof_from_bytes, proof_to_bytes, to_proof, try_from_proof};
 
 use std::ffi::CStr;
 use std::ptr::NonNull;
@@ -75,6 +75,75 @@ pub struct Params {
     pub num_queries: u32,
     pub proof_of_work_bits: u32,
     pub public_degree: i32,
+    /// U2: the internal layer's diagonal d (s_i <- sum + d_i s_i); None =
+    /// (1, 1, 2).  Must be the diagonal of the fork's
+    /// `Poseidon2InternalLayerBls12337<3>`, which [`perm`] instantiates.
+    pub internal_diag: Option<[Val; 3]>,
+    /// U3: the external layer M_E, row-major; None = circ(2, 1, 1).  Must be
+    /// the fork's `Poseidon2ExternalLayerBls12337<3>` matrix.
+    pub external_mds: Option<[Val; 9]>,
+}
+
+impl Params {
+    /// The Poseidon2 constants `Perm::new_from_rng(rounds_f, rounds_p, rng)`
+    /// (`bin/src/main.rs:49`) draws, drawn from `rng` in the same order and
+    /// by the fork's own samplers: `ExternalLayerConstants::new_from_rng`
+    /// (the rounds_f/2 initial, then the rounds_f/2 terminal `[Val; 3]`),
+    /// then rounds_p internal constants.  So
+    /// `perm(&Params::from_rng(8, 22, &mut rng))` is the permutation
+    /// `Perm::new_from_rng(8, 22, &mut rng)` builds from the same rng state,
+    /// and the library proves with exactly those constants.  The one-line
+    /// change at `bin/src/main.rs:49`:
+    /// `let params = p3_hip::Params::from_rng(8, 22, &mut rng); let perm = p3_hip::perm(&params);`
+    pub fn from_rng<R: rand::Rng>(rounds_f: usize, rounds_p: usize, rng: &mut R) -> Params
+    where
+        rand::distributions::Standard: rand::distributions::Distribution<Val> + rand::distributions::Distribution<[Val; 3]>,
+    {
+        use rand::distributions::Standard;
+        let ext = p3_poseidon2::ExternalLayerConstants::<Val, 3>::new_from_rng(rounds_f, rng);
+        let internal: Vec<Val> = (&mut *rng).sample_iter(Standard).take(rounds_p).collect();
+        let mut rc = Vec::with_capacity(3 * rounds_f + rounds_p);
+        for r in ext.get_initial_constants().iter().chain(ext.get_terminal_constants()) {
+            rc.extend_from_slice(r);
+        }
+        rc.extend(internal);
+        Params { rounds_f: rounds_f as u32, rounds_p: rounds_p as u32, round_constants: rc, ..Params::default() }
+    }
+
+    /// `round_constants`, or the library's seeded set (lsp_seeded_setup, U4) when empty
+    pub fn resolved_round_constants(&self) -> Vec<Val> {
+        if !self.round_constants.is_empty() {
+            return self.round_constants.clone();
+        }
+        let n = (3 * self.rounds_f + self.rounds_p) as usize;
+        let (mut a, mut d) = (sys::lsp_fr::default(), sys::lsp_fr::default());
+        let mut rc = vec![sys::lsp_fr::default(); n];
+        let st = unsafe {
+            sys::lsp_seeded_setup(DEFAULT_SEED, self.rounds_f, self.rounds_p, &mut a, &mut d, rc.as_mut_ptr())
+        };
+        check_global(st, "lsp_seeded_setup");
+        unsafe { vals(rc.as_ptr(), n) }
+    }
+}
+
+/// the library's documented seed (U4/U5, "LINEA")
+pub const DEFAULT_SEED: u64 = 0x4C494E4541;
+
+/// `Poseidon2Bls12337<3>` built from exactly `p`'s round constants: the
+/// `Perm` of `bin/src/main.rs:49`, which the Hash, both Mmcs and the
+/// challenger share (`main.rs:50-57,78,88`), so the reference's unchanged
+/// `p3_uni_stark::verify` hashes with the constants the library proved with.
+pub fn perm(p: &Params) -> p3_bls12_377_fr::Poseidon2Bls12337<3> {
+    let rc = p.resolved_round_constants();
+    let half = (p.rounds_f / 2) as usize;
+    let row = |k: usize| -> [Val; 3] { [rc[3 * k], rc[3 * k + 1], rc[3 * k + 2]] };
+    let initial: Vec<[Val; 3]> = (0..half).map(row).collect();
+    let terminal: Vec<[Val; 3]> = (half..2 * half).map(row).collect();
+    let internal = rc[6 * half..].to_vec();
+    p3_bls12_377_fr::Poseidon2Bls12337::<3>::new(
+        p3_poseidon2::ExternalLayerConstants::new(initial, terminal),
+        internal,
+    )
 }
 
 impl Default for Params {
@@ -89,6 +158,8 @@ impl Default for Params {
             num_queries: 33,
             proof_of_work_bits: 0,
             public_degree: 1,
+            internal_diag: None,
+            external_mds: None,
         }
     }
 }
@@ -105,7 +176,9 @@ unsafe impl Sync for Ctx {}
 
 impl Ctx {
     pub fn new(device: i32, p: &Params) -> Ctx {
-        let rc_ptr = if p.round_constants.is_empty() { std::ptr::null() } else { fr_ptr(&p.round_constants) };
+        // lsp_ctx_create needs the constants: the seeded set when none are given
+        let rc = p.resolved_round_constants();
+        let rc_ptr = fr_ptr(&rc);
         let raw_params = sys::lsp_params {
             sbox_degree: p.sbox_degree,
             rounds_f: p.rounds_f,
@@ -116,6 +189,8 @@ impl Ctx {
             num_queries: p.num_queries,
             proof_of_work_bits: p.proof_of_work_bits,
             public_degree: p.public_degree,
+            internal_diag: p.internal_diag.as_ref().map_or(std::ptr::null(), |d| fr_ptr(d)),
+            external_mds: p.external_mds.as_ref().map_or(std::ptr::null(), |m| fr_ptr(m)),
         };
         let mut out: *mut sys::lsp_ctx = std::ptr::null_mut();
         let rc = unsafe { sys::lsp_ctx_create(device, &raw_params, &mut out) };

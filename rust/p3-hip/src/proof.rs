@@ -135,13 +135,78 @@ where
     recast(&m, "lsp_proof -> Proof<SC>")
 }
 
-/// Proof<SC> -> a new lsp_proof handle (free with sys::lsp_proof_free)
-pub fn from_proof<SC>(proof: &Proof<SC>) -> *mut sys::lsp_proof
+/// The flat view (include/lsp.h lsp_proof_view) gives every query the shape
+/// of query 0, and lsp_proof_from_view reads that many elements per query out
+/// of the Vecs built below.  A deserialized (untrusted) Proof<SC> with ragged
+/// queries must therefore be rejected here, before any pointer is handed out.
+fn check_shape(m: &ProofMirror) -> Result<(), String> {
+    let (ov, fp) = (&m.opened_values, &m.opening_proof);
+    let w = ov.trace_local.len();
+    if ov.trace_next.len() != w {
+        return Err(format!("trace_next has {} values, trace_local {w}", ov.trace_next.len()));
+    }
+    let q = ov.quotient_chunks.len();
+    if !q.is_power_of_two() || ov.quotient_chunks.iter().any(|c| c.len() != 1) {
+        return Err("quotient_chunks: need 2^k chunks of one value each".into());
+    }
+    if !fp.final_poly.len().is_power_of_two() {
+        return Err(format!("final_poly length {} is not a power of two", fp.final_poly.len()));
+    }
+    let nr = fp.commit_phase_commits.len();
+    let first = fp.query_proofs.first();
+    let pl = first.and_then(|qp| qp.input_proof.first()).map_or(0, |b| b.opening_proof.len());
+    let fpl: Vec<usize> = first.map_or_else(
+        || vec![0; nr],
+        |qp| qp.commit_phase_openings.iter().map(|s| s.opening_proof.len()).collect(),
+    );
+    for (i, qp) in fp.query_proofs.iter().enumerate() {
+        let bad = |what: &str| Err(format!("query {i}: {what}"));
+        if qp.input_proof.len() != 2 {
+            return bad("needs two batch openings (trace, quotient chunks)");
+        }
+        let (t, qb) = (&qp.input_proof[0], &qp.input_proof[1]);
+        if t.opened_values.len() != 1 || t.opened_values[0].len() != w {
+            return bad("trace row width differs from trace_local");
+        }
+        if qb.opened_values.len() != q || qb.opened_values.iter().any(|r| r.len() != 1) {
+            return bad("quotient row shape differs from quotient_chunks");
+        }
+        if t.opening_proof.len() != pl || qb.opening_proof.len() != pl {
+            return bad("input Merkle path length differs from query 0");
+        }
+        if qp.commit_phase_openings.len() != nr {
+            return bad("commit-phase openings differ from commit_phase_commits");
+        }
+        if qp.commit_phase_openings.iter().zip(&fpl).any(|(s, &l)| s.opening_proof.len() != l) {
+            return bad("FRI path length differs from query 0");
+        }
+    }
+    Ok(())
+}
+
+/// Proof<SC> -> a new lsp_proof handle (free with sys::lsp_proof_free);
+/// Err on a proof whose queries do not share one shape
+pub fn try_from_proof<SC>(proof: &Proof<SC>) -> Result<*mut sys::lsp_proof, String>
 where
     SC: StarkGenericConfig,
     Proof<SC>: Serialize,
 {
     let m: ProofMirror = recast(proof, "Proof<SC> -> lsp_proof");
+    check_shape(&m)?;
+    Ok(view_to_handle(&m))
+}
+
+/// Proof<SC> -> a new lsp_proof handle (free with sys::lsp_proof_free);
+/// panics on a malformed proof (see [`try_from_proof`])
+pub fn from_proof<SC>(proof: &Proof<SC>) -> *mut sys::lsp_proof
+where
+    SC: StarkGenericConfig,
+    Proof<SC>: Serialize,
+{
+    try_from_proof(proof).unwrap_or_else(|e| panic!("from_proof: malformed Proof<SC>: {e}"))
+}
+
+fn view_to_handle(m: &ProofMirror) -> *mut sys::lsp_proof {
     let fp = &m.opening_proof;
     let flat = |xs: &[[Val; 1]]| xs.iter().map(|d| d[0]).collect::<Vec<Val>>();
     let (mut trows, mut tpaths, mut qrows, mut qpaths, mut sibs, mut fpaths) =

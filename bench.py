@@ -69,6 +69,24 @@ NOMINAL_GHZ = 2.4           # MI355X peak engine clock (MI355X_MICROARCH.md)
 SIMDS = 256 * 4             # 256 CUs x 4 SIMD-32 units
 FR_MUL_PER_PERM = 230       # 46 S-boxes x 5 products (x^11), SURVEY 8 conventions
 MAD_PER_FR_MUL = 128        # 8 x 32-bit limbs: 64 product + 64 reduction MADs (the floor the peak assumes)
+FRMUL_PEAK_GPS = SIMDS * 64 / 4 * NOMINAL_GHZ / MAD_PER_FR_MUL  # 307.2 G Fr-mul/s (v_mad_u64_u32: 4 cycles)
+
+
+def _lib_src() -> str:
+    from linea_stark_prover_amd.build import source_hash
+    return source_hash()
+
+
+LIB_SRC = _lib_src()  # the build the committed PMC profiles must match
+VALU_SRC, TRAFFIC_SRC = {}, {}  # where each PMC-derived field came from (or why it is null)
+
+
+def lde_products(h: int, w: int, ncosets: int) -> int:
+    """algorithmic Fr products of one coset LDE of an h x w matrix into
+    ncosets cosets of h: the inverse NTT, one twist per coefficient and coset,
+    and one forward NTT of h per coset"""
+    lg = h.bit_length() - 1
+    return w * ((h // 2) * lg + ncosets * h + ncosets * (h // 2) * lg)
 
 
 def parse(argv=None):
@@ -83,7 +101,11 @@ def parse(argv=None):
                          "wide AIR (4 LogUp lookups + 8 permutation groups of 6+6, W = 184)")
     ap.add_argument("--seed", type=int, default=0x4C494E4541)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-log-n", type=int, default=19, help="CPU-baseline sample size (rows = 2^cpu_log_n)")
+    ap.add_argument("--cpu-log-n", type=int, default=16, help="CPU-baseline sample size (rows = 2^cpu_log_n)")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="CPU-baseline timed runs (median; after 1 warm-up)")
+    ap.add_argument("--shape-leg", default="6",
+                    help="ncols of the extra 2^log_n leg in bench.log's shape (6+6 columns, w = 14, the "
+                         "reference's only measured run, bench.log:18-20); 'none' to skip")
     ap.add_argument("--shard", action="store_true", help="main leg: one proof sharded over the N ranks (C4)")
     ap.add_argument("--comm", choices=["rccl", "gloo"], default="rccl", help="--shard exchange transport")
     ap.add_argument("--shard-leg", default="auto",
@@ -162,6 +184,11 @@ def main():
             batch = {"error": f"{type(e).__name__}: {e}"}
         if rank == 0:
             out["batch"] = batch
+    if world == 1 and args.shape_leg != "none" and args.air == "perm" and not args.shard:
+        try:
+            out["shape_bench_log"] = shape_leg(args, dist, ctx, int(args.shape_leg))
+        except Exception as e:  # the main line is still reported
+            out["shape_bench_log"] = {"error": f"{type(e).__name__}: {e}"}
     if shard_sizes:
         sharded = guarded_shard_leg(args, dist, ctx, shard_sizes, out)
         if rank == 0:
@@ -245,6 +272,8 @@ def main_leg(args, dist, ranks_seen):
         Nr = N // world if shard else N  # LDE rows (Merkle leaves) this rank computes
         lde_bytes = 32 * w * (h + Nr)
         achieved = lde_bytes / (lde_ms * 1e-3) / 1e9
+        lde_frmul = lde_products(h, w, Nr // h)
+        frmul_gps = lde_frmul / (lde_ms * 1e-3) / 1e9
         merkle_ms = phases.get("merkle tree", float("nan"))
         trace_perms = Nr * ((w + 1) // 2) + (Nr - 1)
         valu_achieved = trace_perms / (merkle_ms * 1e-3) / 1e6
@@ -276,10 +305,20 @@ def main_leg(args, dist, ranks_seen):
                                        f"replicas{world}" if world > 1 else "single-gpu")},
             "verified": bool(verified),
             "phases_ms": {k: round(v, 3) for k, v in phases.items()},
+            "lib_src_sha16": LIB_SRC,
             "roofline": {"bound": "hbm", "kernel": "coset_lde_batch (trace, w x 2^log_n -> 8x)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": lde_traffic(args.log_n, w),
+                         "traffic_source": TRAFFIC_SRC.get((args.log_n, w)),
                          "valu_issue": valu_issue(["k_ntt_rm"]),
+                         "valu_issue_source": VALU_SRC.get("src"),
+                         "frmul_frac": frmul_gps / FRMUL_PEAK_GPS,
+                         "frmul": {"products_per_call": lde_frmul, "achieved_g_per_s": frmul_gps,
+                                   "peak_g_per_s": FRMUL_PEAK_GPS,
+                                   "count": "w x [(h/2) log2 h (inverse) + N (coset twists) + (N/2) log2 h "
+                                            "(8 forward coset NTTs of h)] Fr products",
+                                   "peak_basis": "1024 SIMDs x 64 lanes / 4 cycles per v_mad_u64_u32 x 2.4 GHz / "
+                                                 "128 MADs per 8 x 32-bit Montgomery product"},
                          "note": "VALU-bound: valu_issue = share of SIMD cycles issuing VALU in the NTT passes "
                                  "(PMC SQ_ACTIVE_INST_VALU, profiles/*_valu_pmc.json); HBM frac is low by design",
                          "algorithmic_bytes": lde_bytes, "ms": lde_ms},
@@ -305,7 +344,8 @@ def main_leg(args, dist, ranks_seen):
                               "fr_mul_achieved_g_per_s": valu_achieved * FR_MUL_PER_PERM / 1e3,
                               "fr_mul_peak_g_per_s": peak["gfrmul_per_s"] if peak else None,
                               "calibrated_register_resident_mperm_per_s": ctx.calibrate_poseidon2(),
-                              "valu_issue": valu_issue(["k_hash_rows1<11u, false>", "k_merkle_level<11u, false>"]),
+                              "valu_issue": valu_issue(["k_hash_rows1<11u, 1>", "k_merkle_level<11u, 1>"]),
+                              "valu_issue_source": VALU_SRC.get("src"),
                               "perms": trace_perms, "fr_mul_per_perm": FR_MUL_PER_PERM, "ms": merkle_ms},
         }
         if world == 1 and not shard and args.inflight > 1:
@@ -373,6 +413,39 @@ def batch_leg(args, dist, ctx, sizes):
     return {"runs": runs}
 
 
+def shape_leg(args, dist, ctx, ncols):
+    """The shape of the reference's only measured run (bench.log:1-20: a
+    permutation over 6 'from' + 6 'to' columns, w = 14, 2^19 rows, 8 quotient
+    chunks; 342 s on its CPU, bench.log:18), same K/W as the main leg, trace
+    resident in HBM (device-generated)."""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import StarkConfig
+    from linea_stark_prover_amd.replicas import timed_steps
+    import numpy as np
+    cfg = StarkConfig(seed=args.seed)
+    a, d, _ = cfg.seeded()
+    pub = np.concatenate([a, d])
+    air = permutation_air(ncols)
+    w, h = 2 * ncols + 2, 1 << args.log_n
+    dtrace = ctx.gen_permutation_trace_device(args.log_n, ncols, a, d, seed=args.seed)
+    step_s = []
+    try:
+        step = lambda: ctx.prove(dtrace, air, pub, h, w)  # noqa: E731
+        elapsed, proof = timed_steps(step, args.steps, max(args.warmup, 1), dist, sync=ctx.synchronize,
+                                     step_times=step_s)
+    finally:
+        ctx.dev_free(dtrace)
+    t = elapsed / args.steps
+    return {"workload": f"{ncols}x{ncols} permutation AIR, 2^{args.log_n} rows (w={w}, q="
+                        f"{1 << air_log_q(air, cfg)}): the shape of bench.log:18-20",
+            "steps": args.steps, "warmup": max(args.warmup, 1), "prove_time_s": t,
+            "prove_time_median_s": statistics.median(step_s) if step_s else None,
+            "value": h / t, "unit": "trace-rows/s", "verified": bool(ctx.verify(proof, air, pub)),
+            "phases_ms": {k: round(v, 3) for k, v in ctx.last_timings()},
+            "reference_s": 342.0, "reference_source": "bench.log:18 (6+6 columns, w = 14, 2^19 rows, CPU)",
+            "speedup_vs_reference": 342.0 / t if args.log_n == 19 else None}
+
+
 def shard_leg_sizes(args, world):
     if args.shard_leg == "none" or args.shard or args.air != "perm":
         return []
@@ -381,10 +454,16 @@ def shard_leg_sizes(args, world):
     return [int(x) for x in args.shard_leg.split(",") if x]
 
 
-def guarded_shard_leg(args, dist, ctx, sizes, out):
+WATCHDOG_EXIT = 3  # exit status of every rank whose sharded leg hung
+
+
+def guarded_shard_leg(args, dist, ctx, sizes, out, leg=None):
     """Run the C4 leg under a per-rank watchdog: if any collective hangs, rank
-    0 still prints the main line (with the failure noted) and every rank exits."""
+    0 still prints the main line (with the failure noted) and every rank exits
+    with WATCHDOG_EXIT, so the run's status reports the hang
+    (tests/test_replicas.py simulates one)."""
     done = threading.Event()
+    leg = leg or shard_leg
 
     def watchdog():
         if done.wait(args.shard_timeout):
@@ -392,11 +471,12 @@ def guarded_shard_leg(args, dist, ctx, sizes, out):
         if dist.rank == 0 and out is not None:
             out["sharded"] = {"error": f"sharded leg exceeded {args.shard_timeout:.0f} s on rank 0; abandoned"}
             print(json.dumps(out), flush=True)
-        os._exit(0 if dist.rank == 0 else 3)
+        sys.stdout.flush()
+        os._exit(WATCHDOG_EXIT)
 
     threading.Thread(target=watchdog, daemon=True).start()
     try:
-        return shard_leg(args, dist, ctx, sizes)
+        return leg(args, dist, ctx, sizes)
     except Exception as e:  # the main line is still reported
         return {"error": f"{type(e).__name__}: {e}"}
     finally:
@@ -547,16 +627,25 @@ def valu_issue(kernels):
     """Time-weighted VALU issue share of the named kernels from the committed
     PMC passes (tools/pmc_valu.sh -> profiles/*_valu_pmc.json): SIMD cycles
     with a VALU instruction issuing (SQ_ACTIVE_INST_VALU over all waves) /
-    (1024 SIMDs x kernel cycles); None if absent."""
+    (1024 SIMDs x kernel cycles).  Only a profile stamped with this library's
+    source hash counts (lib_src_sha16); else None, with the reason in
+    VALU_SRC."""
     import glob
-    d = None
+    d, src, stale = None, None, []
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu_pmc.json"))):
         try:
-            d = json.load(open(path))
+            x = json.load(open(path))
         except (OSError, ValueError):
             continue
+        if x.get("lib_src_sha16") == LIB_SRC:
+            d, src = x, os.path.relpath(path, ROOT)
+        else:
+            stale.append(os.path.basename(path))
     if not d:
+        VALU_SRC["src"] = (f"null: no profiles/*_valu_pmc.json measured on this build (lib_src_sha16 {LIB_SRC}; "
+                           f"{len(stale)} older profile(s) skipped)")
         return None
+    VALU_SRC["src"] = src
     ks = [v for k, v in d["kernels"].items() if any(k.startswith(p) for p in kernels)]
     ms = sum(v["ms"] for v in ks)
     return round(sum(v["valu_issue"] * v["ms"] for v in ks) / ms, 3) if ms else None
@@ -565,16 +654,24 @@ def valu_issue(kernels):
 def lde_traffic(log_n, w):
     """HBM bytes per coset_lde_batch from the rocprofv3 PMC passes of
     tools/pmc_round.sh (FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), kept in
-    profiles/; None when no measurement matches this size."""
+    profiles/; None when no measurement of this size was made on this build
+    (lib_src_sha16), with the reason in TRAFFIC_SRC."""
     import glob
-    best = None
+    best, stale = None, 0
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_lde_traffic.json"))):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
         if d.get("h") == (1 << log_n) and d.get("w") == w:
-            best = d["traffic_bytes"]
+            if d.get("lib_src_sha16") == LIB_SRC:
+                best = d["traffic_bytes"]
+                TRAFFIC_SRC[(log_n, w)] = os.path.relpath(path, ROOT)
+            else:
+                stale += 1
+    if best is None:
+        TRAFFIC_SRC[(log_n, w)] = (f"null: no profiles/*_lde_traffic.json of 2^{log_n} x {w} measured on this build "
+                                   f"(lib_src_sha16 {LIB_SRC}; {stale} older profile(s) skipped)")
     return best
 
 
@@ -601,26 +698,34 @@ def cpu_share() -> int:
 
 
 def cpu_baseline(args):
-    """The oracle's C restatement proving the headline workload (2^cpu_log_n
-    rows) on the host (test infrastructure used only as the reported
-    baseline), one thread per core of this process's CPU share."""
+    """The oracle's C restatement proving the headline workload's AIR
+    (2^cpu_log_n rows) on the host (test infrastructure used only as the
+    reported baseline), one thread per core of this process's CPU share: one
+    warm-up, then the median of --cpu-runs timed proofs."""
     from oracle import cref
     cref.build()
     threads = cpu_share()
     p = cref.setup(args.seed)
     tb, w = cref.gen_perm_trace(p, args.cpu_log_n, args.ncols, seed=args.seed)
-    t = time.perf_counter()
-    cref.prove(p, tb, 1 << args.cpu_log_n, w, cref.perm_air(args.ncols), nthreads=threads)
-    dt = time.perf_counter() - t
+    air = cref.perm_air(args.ncols)
+    cref.prove(p, tb, 1 << args.cpu_log_n, w, air, nthreads=threads)  # warm-up
+    ts = []
+    for _ in range(max(args.cpu_runs, 1)):
+        t = time.perf_counter()
+        cref.prove(p, tb, 1 << args.cpu_log_n, w, air, nthreads=threads)
+        ts.append(time.perf_counter() - t)
+    dt = statistics.median(ts)
     try:
         nproc = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
     except (OSError, ValueError):
         nproc = None
     return {"value": (1 << args.cpu_log_n) / dt, "unit": "trace-rows/s", "cores": threads, "kind": "port",
-            "seconds": dt, "nproc": nproc, "machine_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+            "seconds": dt, "seconds_runs": [round(x, 3) for x in ts], "warmup": 1, "nproc": nproc,
+            "machine_cpus": os.cpu_count(), "cpu_model": cpu_model(),
             "sample": f"oracle/lsp_oracle.c full prove, {args.ncols}x{args.ncols} permutation AIR at "
-                      f"2^{args.cpu_log_n} rows (the headline workload, same conventions/seed), {threads} threads "
-                      f"= this process's CPU share (affinity / OMP_NUM_THREADS)"}
+                      f"2^{args.cpu_log_n} rows (same AIR, conventions and seed as the headline; a bounded "
+                      f"sample of its 2^{args.log_n}-row workload), median of {len(ts)} runs after 1 warm-up, "
+                      f"{threads} threads = this process's CPU share (affinity / OMP_NUM_THREADS)"}
 
 
 if __name__ == "__main__":

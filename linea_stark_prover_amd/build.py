@@ -33,6 +33,24 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno
           "-Wno-unused-variable", "-I", os.path.join(ROOT, "include")]
 
 
+def source_hash() -> str:
+    """sha256 (16 hex digits) of everything the library is built from: the
+    csrc/ sources, include/lsp.h and the compile flags.  Profiles measured on
+    one build (PMC traffic, VALU issue) carry it, and bench.py uses a profile
+    only when it matches the library being benched."""
+    import hashlib
+    hsh = hashlib.sha256()
+    files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp", ".hpp", ".inc")))
+    for f in files:
+        hsh.update(f.encode())
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            hsh.update(fh.read())
+    with open(os.path.join(ROOT, "include", "lsp.h"), "rb") as fh:
+        hsh.update(fh.read())
+    hsh.update(" ".join(CFLAGS[:-1] + [ARCH]).encode())
+    return hsh.hexdigest()[:16]
+
+
 def _headers():
     return [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".inc"))] + \
         [os.path.join(ROOT, "include", "lsp.h")]

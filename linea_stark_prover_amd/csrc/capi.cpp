@@ -853,6 +853,7 @@ int lsp_prove_sharded(lsp_ctx* ctx, const lsp_fr* trace, size_t h, size_t w, con
 int lsp_proof_serialize(const lsp_proof* p, uint8_t* buf, size_t cap, size_t* len) {
     return guarded(nullptr, [&] {
         LSP_REQUIRE(p && len, LSP_E_ARG, "null");
+        std::lock_guard<std::mutex> g(p->cache_mu);
         if (p->wire.empty()) p->wire = serialize(*p);  // a size query and the copy serialize once
         const std::vector<uint8_t>& b = p->wire;
         *len = b.size();
@@ -910,8 +911,12 @@ int lsp_verify(const lsp_ctx* ctx, const int32_t* air, size_t air_len, const lsp
 
 int lsp_last_timings(const lsp_ctx* ctx, double* ms, const char** names, size_t cap, size_t* n) {
     if (!ctx || !n) return LSP_E_ARG;
+    // resolve_timings writes the context's timing state, which lsp_prove writes
+    // too: the context's mutex serialises them (a Rust Ctx is Sync)
+    lsp_ctx* c = const_cast<lsp_ctx*>(ctx);
+    std::lock_guard<std::mutex> g(c->mu);
     try {
-        lsp::resolve_timings(const_cast<lsp_ctx*>(ctx));  // the events are the context's own
+        lsp::resolve_timings(c);  // the events are the context's own
     } catch (...) {
         return LSP_E_HIP;
     }
@@ -925,6 +930,7 @@ int lsp_last_timings(const lsp_ctx* ctx, double* ms, const char** names, size_t 
 
 int lsp_last_spans(const lsp_ctx* ctx, const char** lines, size_t cap, size_t* n) {
     if (!ctx || !n) return LSP_E_ARG;
+    std::lock_guard<std::mutex> g(const_cast<lsp_ctx*>(ctx)->mu);  // spans are rewritten by lsp_prove
     *n = ctx->spans.size();
     for (size_t i = 0; i < ctx->spans.size() && i < cap; ++i)
         if (lines) lines[i] = ctx->spans[i].c_str();

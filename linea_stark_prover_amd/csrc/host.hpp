@@ -191,6 +191,9 @@ struct lsp_proof {
     lsp::Fr troot, qroot, pow_w;
     std::vector<lsp::Fr> tl, tn, qc, roots, final_poly;
     std::vector<lsp::lsp_query> queries;
+    // caches filled on first use by calls that take a const proof (a proof may
+    // be shared across threads, e.g. rayon tasks): built under cache_mu
+    mutable std::mutex cache_mu;
     mutable std::vector<uint8_t> wire;  // serialize() result, cached by lsp_proof_serialize
     mutable std::shared_ptr<void> view_cache;  // flat arrays behind lsp_proof_view (proof.cpp)
 };

@@ -82,6 +82,8 @@ __global__ __launch_bounds__(256) void k_interp_partial(const Fr* __restrict__ M
     }
 }
 
+static_assert(sizeof(F29) == 36, "reduce_rows_scratch (kernels.hpp) assumes 36-byte F29");
+
 // one workgroup per column: strided partial sums, then a tree in LDS
 __global__ __launch_bounds__(256) void k_sum_partials(const Fr* __restrict__ partial, uint32_t nb, uint32_t w,
                                                       Fr* __restrict__ out) {
@@ -106,20 +108,36 @@ __global__ __launch_bounds__(256) void k_sum_partials(const Fr* __restrict__ par
 // per-row factor (the inverse denominators) once per row; sums stay lazily
 // reduced (at most 3 products per limb-wise sum, then the LDS-table
 // reduction).  The result is canonical.
+// the per-call constants of k_reduce_rows in their kernel form: apw[0..w] and
+// apw[2w..2w+q) in the 29-bit form, then ryq[0..q) as limbs (ark form)
+__device__ __forceinline__ F29 rr_const(const ReduceArgs& a, uint32_t k) {
+    if (k <= a.w) return f29_from_fr(a.apw[k]);
+    if (k < a.w + 1 + a.q) return f29_from_fr(a.apw[2 * a.w + (k - a.w - 1)]);
+    return f29_repack_in(a.ryq[k - a.w - 1 - a.q]);
+}
+
+// wide matrices (GLB, the constants beyond the LDS): converted once into global memory
+__global__ __launch_bounds__(256) void k_reduce_consts(ReduceArgs a) {
+    const size_t k = gtid();
+    if (k < a.w + 1 + 2 * (size_t)a.q) a.consts29[k] = rr_const(a, (uint32_t)k);
+}
+
+// GLB: the constants come from a.consts29 (k_reduce_consts) instead of the
+// workgroup's LDS -- for w + 2q beyond the LDS (about 4,400 columns)
+template <bool GLB>
 __global__ __launch_bounds__(256) void k_reduce_rows(ReduceArgs a) {
     extern __shared__ uint4 rr_lds[];
     uint4* qt = rr_lds;                                               // 3 * F29_QTAB_N
-    F29* apw29 = reinterpret_cast<F29*>(rr_lds + 3 * F29_QTAB_N);   // apw[0..w], apw[2w..2w+q): 29-bit form
-    F29* ryq_l = apw29 + a.w + 1 + a.q;                              // ryq[j] as limbs (ark form)
+    const F29* apw29;  // apw[0..w], apw[2w..2w+q): 29-bit form
     f29_qtab_init(qt);
-    for (uint32_t k = threadIdx.x; k < a.w + 1 + 2 * a.q; k += blockDim.x) {
-        if (k <= a.w)
-            apw29[k] = f29_from_fr(a.apw[k]);
-        else if (k < a.w + 1 + a.q)
-            apw29[k] = f29_from_fr(a.apw[2 * a.w + (k - a.w - 1)]);
-        else
-            ryq_l[k - a.w - 1 - a.q] = f29_repack_in(a.ryq[k - a.w - 1 - a.q]);
+    if constexpr (GLB) {
+        apw29 = a.consts29;
+    } else {
+        F29* c = reinterpret_cast<F29*>(rr_lds + 3 * F29_QTAB_N);
+        for (uint32_t k = threadIdx.x; k < a.w + 1 + 2 * a.q; k += blockDim.x) c[k] = rr_const(a, k);
+        apw29 = c;
     }
+    const F29* ryq_l = apw29 + a.w + 1 + a.q;  // ryq[j] as limbs (ark form)
     __syncthreads();
     const size_t i = gtid();
     if (i >= a.n) return;
@@ -227,9 +245,16 @@ hipError_t launch_sum_partials(const Fr* partial, uint32_t nb, uint32_t w, Fr* o
 }
 
 hipError_t launch_reduce_rows(const ReduceArgs& a, hipStream_t st) {
-    const size_t lds = 3 * F29_QTAB_N * sizeof(uint4) + (a.w + 1 + 2 * (size_t)a.q) * sizeof(F29);
-    if (lds > 64 * 1024) return hipErrorInvalidValue;  // w + 2q up to ~1800 columns
-    hipLaunchKernelGGL(k_reduce_rows, dim3(nblocks(a.n, 256)), dim3(256), lds, st, a);
+    const size_t qtab = 3 * F29_QTAB_N * sizeof(uint4);
+    const size_t nconst = a.w + 1 + 2 * (size_t)a.q;
+    const size_t lds = qtab + nconst * sizeof(F29);
+    if (lds <= REDUCE_ROWS_LDS_MAX) {
+        hipLaunchKernelGGL(k_reduce_rows<false>, dim3(nblocks(a.n, 256)), dim3(256), lds, st, a);
+        return hipGetLastError();
+    }
+    if (!a.consts29) return hipErrorInvalidValue;  // the caller must pass the global scratch (reduce_rows_scratch)
+    hipLaunchKernelGGL(k_reduce_consts, dim3(nblocks(nconst, 256)), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_reduce_rows<true>, dim3(nblocks(a.n, 256)), dim3(256), qtab, st, a);
     return hipGetLastError();
 }
 

@@ -176,7 +176,16 @@ struct ReduceArgs {
     const Fr* ryq;     // opened value of each quotient chunk at zeta (q)
     Fr* out;           // N
     size_t n;
+    F29* consts29 = nullptr;  // global scratch of reduce_rows_scratch(w, q) F29 (needed only beyond the LDS)
 };
+// the reduce-rows constants stay in the workgroup's LDS up to this many bytes
+// (gfx950: 160 KiB per workgroup), i.e. w + 2q <= ~4,400 columns; wider
+// matrices keep them in global memory (ReduceArgs::consts29)
+constexpr size_t REDUCE_ROWS_LDS_MAX = 160 * 1024;
+inline size_t reduce_rows_scratch(uint32_t w, uint32_t q) {
+    const size_t lds = 3 * 64 * 16 + (w + 1 + 2 * (size_t)q) * 36;
+    return lds <= REDUCE_ROWS_LDS_MAX ? 0 : w + 1 + 2 * (size_t)q;
+}
 hipError_t launch_reduce_rows(const ReduceArgs& a, hipStream_t st);
 // one matrix opened at npts points (the generic reduce of TwoAdicFriPcs::open):
 // ro[i] += sum_p (offys[p] - off[p] * sum_c apw[c] M[i][c]) * inv[p*n + i]

@@ -181,6 +181,9 @@ struct Flat {
 }  // namespace
 
 void proof_view(const lsp_proof& p, lsp_proof_view* v) {
+    // built once, under the proof's cache mutex; never replaced afterwards, so
+    // pointers handed out stay valid until lsp_proof_free
+    std::lock_guard<std::mutex> g(p.cache_mu);
     if (!p.view_cache) {
         auto f = std::make_shared<Flat>();
         const size_t nq = p.queries.size(), nr = p.roots.size();
@@ -235,8 +238,12 @@ void proof_view(const lsp_proof& p, lsp_proof_view* v) {
 }
 
 lsp_proof* proof_from_view(const lsp_proof_view& v) {
+    // final_poly_len: a power of two (1 << log_final_poly_len) <= 2^20, the only
+    // lengths the wire format's reader accepts, so every view that builds a
+    // handle serializes to bytes lsp_proof_deserialize reads back
     if (v.width == 0 || v.width > (1u << 20) || v.log_quotient_chunks > 20 || v.degree_bits > 40 ||
-        v.num_fri_rounds > 64 || v.input_path_len > 64 || v.final_poly_len == 0)
+        v.num_fri_rounds > 64 || v.input_path_len > 64 || v.final_poly_len == 0 || v.final_poly_len > (1u << 20) ||
+        (v.final_poly_len & (v.final_poly_len - 1)) != 0)
         throw LspError(LSP_E_ARG, "proof view out of range");
     const size_t w = v.width, q = (size_t)1 << v.log_quotient_chunks, nr = v.num_fri_rounds, pl = v.input_path_len;
     LSP_REQUIRE(v.trace_commit && v.quotient_commit && v.pow_witness && v.trace_local && v.trace_next &&

@@ -760,6 +760,8 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         ra.ryq = dapw + napw;
         ra.out = fvec;
         ra.n = S;
+        if (const size_t nsc = reduce_rows_scratch(ra.w, ra.q))  // constants beyond the LDS: global
+            ra.consts29 = (F29*)ctx->buf("o_rr_consts", nsc * sizeof(F29));
         LSP_HIP(launch_reduce_rows(ra, st));
         T.end("reduce rows");
 

@@ -594,7 +594,7 @@ void lo_lde_point(size_t h, uint32_t added_bits, const lo_fr *shift, uint64_t j,
 }
 
 /* -------------------------------------------------------------------- AIR */
-#define MAXC 256
+#define MAXC 4096
 #define MAXT 32
 #define MAXCFG 64
 typedef struct {

@@ -35,8 +35,10 @@ impl TwoAdicSubgroupDft<Val> for HipDft {
     type Evaluations = BitReversedMatrixView<RowMajorMatrix<Val>>;
 
     fn dft_batch(&self, mat: RowMajorMatrix<Val>) -> Self::Evaluations {
-        // a plain DFT is not on the prover's path (only coset_lde_batch is):
-        // the CPU radix-2 DIT gives the identical, unique result
+        // a plain coefficient DFT is not on the prover's path (only
+        // coset_lde_batch is) and the library exports no coefficient-input
+        // transform: this runs the CPU radix-2 DIT (identical, unique result)
+        // and costs CPU time for a caller that does use it
         Radix2DitParallel::<Val>::default().dft_batch(mat)
     }
 

@@ -69,6 +69,8 @@ impl Mmcs<Val> for HipMmcs {
         assert!(!inputs.is_empty(), "HipMmcs::commit of no matrices");
         let height = inputs[0].height();
         assert!(inputs.iter().all(|m| m.height() == height), "HipMmcs commits matrices of one height");
+        // any M: Matrix -> one contiguous host copy per matrix for the upload
+        // (host memory holds the matrices twice while this runs)
         let staged: Vec<Vec<Val>> = inputs.iter().map(|m| m.rows().flatten().collect()).collect();
         let ptrs: Vec<*const sys::lsp_fr> = staged.iter().map(|v| fr_ptr(v)).collect();
         let widths: Vec<usize> = inputs.iter().map(|m| m.width()).collect();

@@ -27,3 +27,23 @@ def test_wide_prove_matches_oracle_2e12(gpu_ctx, oracle_lib):
     got = gpu_ctx.prove(tr, air, pub)
     p = oracle_lib.setup()
     assert got == oracle_lib.prove(p, tr.ctypes.data, 1 << 12, tr.shape[1], air.descriptor())
+
+
+@pytest.mark.parametrize("ncols", [1023, 2300])
+def test_very_wide_trace_matches_oracle(product_lib, oracle_lib, ncols):
+    """w = 2048 and w = 4602: the reduce-rows constants beyond 64 KiB of LDS
+    (in LDS up to gfx950's 160 KiB, in global memory beyond), which round 2's
+    kernel refused (review: any width the reference handles must prove).
+    Public degree 0 keeps q = 2 at this width."""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import Context, StarkConfig
+    log_n = 4
+    p = oracle_lib.setup()
+    tb, w = oracle_lib.gen_perm_trace(p, log_n, ncols)
+    exp = oracle_lib.prove(p, tb, 1 << log_n, w, oracle_lib.perm_air(ncols), public_degree=0)
+    trace = np.frombuffer(tb.raw, dtype=np.uint64).reshape(1 << log_n, w, 4).copy()
+    pub = np.concatenate([np.array(p.alpha, np.uint64).reshape(1, 4), np.array(p.delta, np.uint64).reshape(1, 4)])
+    with Context(StarkConfig(public_degree=0)) as ctx:
+        got = ctx.prove(trace, permutation_air(ncols), pub)
+        assert got == exp
+        assert ctx.verify(got, permutation_air(ncols), pub)

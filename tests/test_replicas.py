@@ -94,3 +94,42 @@ def test_world_size_mismatch_is_an_error():
     r = _bench(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2
     assert "refusing" in json.loads(r.stdout.strip().splitlines()[-1])["error"]
+
+
+def test_hung_sharded_leg_exits_nonzero():
+    """bench.py's sharded-leg watchdog: a leg that never returns (a hung
+    collective) still gets the main line printed, with the error noted, and the
+    process exits with a non-zero status -- a driver reading the exit code sees
+    the hang (round-2 review item 6)."""
+    import json
+    code = textwrap.dedent(f"""
+        import sys, time, types
+        sys.path.insert(0, {ROOT!r})
+        sys.argv = ["bench.py"]
+        import bench
+        args = types.SimpleNamespace(shard_timeout=1.0)
+        dist = types.SimpleNamespace(rank=0)
+        out = {{"metric": "m", "value": 1.0}}
+        bench.guarded_shard_leg(args, dist, None, [24], out, leg=lambda *a: time.sleep(60))
+        print("not reached")
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    sys.path.insert(0, ROOT)
+    import bench
+    assert r.returncode == bench.WATCHDOG_EXIT != 0, (r.returncode, r.stderr[-2000:])
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert "exceeded" in line["sharded"]["error"] and line["value"] == 1.0
+    assert "not reached" not in r.stdout
+
+
+def test_bench_helpers():
+    """frmul count of the trace LDE and the stamp check of PMC profiles"""
+    sys.path.insert(0, ROOT)
+    import bench
+    # 2^19 x 8 into 8 cosets: (2^18 * 19 + 8 * 2^19 + 8 * 2^18 * 19) * 8 products (~0.39 G)
+    assert bench.lde_products(1 << 19, 8, 8) == 8 * ((1 << 18) * 19 + 8 * (1 << 19) + 8 * (1 << 18) * 19)
+    assert abs(bench.FRMUL_PEAK_GPS - 307.2) < 1e-9
+    assert len(bench.LIB_SRC) == 16
+    # a profile from another build is never used: null plus the reason
+    bench.lde_traffic(5, 3)
+    assert bench.TRAFFIC_SRC[(5, 3)].startswith("null")

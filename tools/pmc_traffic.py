@@ -3,7 +3,10 @@ tools/pmc_round.sh (FETCH_SIZE and WRITE_SIZE in separate passes, KB units).
 gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE reports half the bytes
 of wide coalesced streaming reads -> doubled; WRITE_SIZE taken as is.
 Writes a JSON summary for the last (steady-state) LDE call."""
-import csv, json, sys
+import csv, json, os, sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from linea_stark_prover_amd.build import source_hash
 
 def per_dispatch(path):
     out = {}
@@ -47,5 +50,6 @@ res = {"kernel": "coset_lde_batch (row-major: inverse DIT pass(es), the fused in
        "per_kernel": [{"dispatch": k, "kernel": fetch[k][0].replace('lsp::(anonymous namespace)::', '').replace('void ', '').split('(')[0],
                        "fetch_bytes_x2": fetch[k][1] * 2048, "write_bytes": write.get(k, [0, 0])[1] * 1024}
                       for k in kern],
-       "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE separate passes on tools/lde_probe.py; FETCH x2 (gfx950)"}
+       "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE separate passes on tools/lde_probe.py; FETCH x2 (gfx950)",
+       "lib_src_sha16": source_hash()}
 print(json.dumps(res, indent=1))

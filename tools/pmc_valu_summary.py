@@ -47,7 +47,10 @@ for name, c in agg.items():
 rows.sort(reverse=True)
 if len(sys.argv) > 2:  # JSON for bench.py (profiles/*_valu_pmc.json)
     import json
-    json.dump({"method": "rocprofv3 --pmc passes (tools/pmc_valu.sh) over tools/time_prove.py 19; "
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from linea_stark_prover_amd.build import source_hash
+    json.dump({"lib_src_sha16": source_hash(),
+               "method": "rocprofv3 --pmc passes (tools/pmc_valu.sh) over tools/time_prove.py 19; "
                          "valu_issue = SQ_ACTIVE_INST_VALU x 4 (all waves) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): "
                          "the share of SIMD cycles issuing VALU; valu_issue_x4 = SQ_INSTS_VALU x 4 / (same) "
                          "(every instruction at the MAD's 4 cycles, r01's measure, reads > 1 for 2-cycle-heavy "

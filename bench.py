@@ -124,6 +124,9 @@ def parse(argv=None):
     ap.add_argument("--batch-leg-steps", type=int, default=2)
     ap.add_argument("--device", type=int, default=None, help="GPU of this rank (default: LOCAL_RANK mod #GPUs)")
     ap.add_argument("--dump-proof", default=None, help="rank 0 writes the last proof here")
+    ap.add_argument("--dump-comm-schedule", default=None,
+                    help="--shard --comm gloo: every rank writes the collectives its communicator carried, in "
+                         "order, to <this>.<rank>.json")
     ap.add_argument("--inflight", type=int, default=3,
                     help="also measure P independent proofs in flight on the GPU (P contexts/streams, "
                          "reported as the separate 'inflight' field, never as value); 0 or 1 disables")
@@ -261,6 +264,10 @@ def main_leg(args, dist, ranks_seen):
     if rank == 0 and args.dump_proof and proof is not None:
         with open(args.dump_proof, "wb") as f:
             f.write(proof)
+    comm = getattr(ctx, "_comm", None)
+    if args.dump_comm_schedule and comm is not None:
+        with open(f"{args.dump_comm_schedule}.{rank}.json", "w") as f:
+            json.dump({"rank": rank, "world": world, "schedule": comm.schedule}, f)
 
     out = None
     if rank == 0:

@@ -254,6 +254,18 @@ int lsp_ctx_attach_comm_ops(lsp_ctx *ctx, const lsp_comm_ops *ops);
 int lsp_comm_rccl_unique_id(uint8_t id[128]);
 int lsp_ctx_attach_rccl(lsp_ctx *ctx, const uint8_t id[128], int rank, int size);
 int lsp_ctx_detach_comm(lsp_ctx *ctx);
+/* Rehearsal transport: this context plays rank `rank` of a `size`-rank
+ * lsp_prove_sharded on its one GPU, every peer's part of an exchange
+ * fabricated locally (allgather slots of other ranks = a copy of this rank's
+ * payload, broadcasts from other roots = zeros).  The proof is NOT valid; the
+ * call measures one rank's device memory and phase times at full size (e.g.
+ * BASELINE configs[3], 2^26 rows over 8 GPUs, one rank at a time on one GPU;
+ * tools/rank_rehearsal.py). */
+int lsp_ctx_attach_loopback(lsp_ctx *ctx, int rank, int size);
+/* device memory of the context: pool_bytes = its grow-only buffer pool (the
+ * high-water mark of its working set), device_used / device_total =
+ * hipMemGetInfo of its GPU */
+int lsp_ctx_mem_stats(lsp_ctx *ctx, size_t *pool_bytes, size_t *device_used, size_t *device_total);
 /* collective check of the attached communicator: an allgather and a
  * broadcast of known patterns (LSP_E_STATE on wrong data) */
 int lsp_comm_selftest(lsp_ctx *ctx);

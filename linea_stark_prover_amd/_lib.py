@@ -105,6 +105,9 @@ _SIGS = {
     "lsp_comm_rccl_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
     "lsp_ctx_attach_rccl": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
     "lsp_ctx_detach_comm": (ctypes.c_int, [ctypes.c_void_p]),
+    "lsp_ctx_attach_loopback": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "lsp_ctx_mem_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
+                                         ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]),
     "lsp_comm_selftest": (ctypes.c_int, [ctypes.c_void_p]),
     "lsp_comm_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "lsp_prove_sharded": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,

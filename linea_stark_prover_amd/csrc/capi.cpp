@@ -770,6 +770,30 @@ int lsp_ctx_attach_comm_ops(lsp_ctx* ctx, const lsp_comm_ops* ops) {
     });
 }
 
+int lsp_ctx_attach_loopback(lsp_ctx* ctx, int rank, int size) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && size >= 1 && rank >= 0 && rank < size, LSP_E_ARG, "bad rank / size");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        delete ctx->comm;
+        ctx->comm = new LoopbackComm(rank, size);
+    });
+}
+
+int lsp_ctx_mem_stats(lsp_ctx* ctx, size_t* pool_bytes, size_t* device_used, size_t* device_total) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && pool_bytes && device_used && device_total, LSP_E_ARG, "null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        size_t pool = 0;
+        for (auto& kv : ctx->pool) pool += kv.second.cap;
+        *pool_bytes = pool;
+        size_t fr = 0, tot = 0;
+        LSP_HIP(hipMemGetInfo(&fr, &tot));
+        *device_used = tot - fr;
+        *device_total = tot;
+    });
+}
+
 int lsp_comm_rccl_unique_id(uint8_t id[128]) {
     return guarded(nullptr, [&] {
         LSP_REQUIRE(id, LSP_E_ARG, "null id");

@@ -53,6 +53,29 @@ struct SoloComm : Comm {
     void bcast(lsp_ctx*, void*, size_t, int) override {}
 };
 
+// Rehearsal of ONE rank of a G-rank proof on one GPU (lsp_ctx_attach_loopback):
+// rank g runs its own share of every phase at full size, and the peers' parts
+// of each exchange are fabricated locally -- allgather slots of other ranks get
+// a copy of this rank's payload, a broadcast from another root leaves zeros (a
+// valid field element).  The proof it returns is not a valid proof; what it
+// measures is rank g's device memory and per-phase time at the real shapes,
+// e.g. one rank of BASELINE configs[3] (2^26 rows over 8 GPUs) on a single GPU.
+struct LoopbackComm : Comm {
+    LoopbackComm(int r, int n) {
+        rank = r;
+        size = n;
+    }
+    void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
+        for (int r = 0; r < size; ++r) {
+            void* dst = (char*)recv + (size_t)r * bytes;
+            if (dst != send) LSP_HIP(hipMemcpyAsync(dst, send, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+        }
+    }
+    void bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) override {
+        if (root != rank) LSP_HIP(hipMemsetAsync(buf, 0, bytes, ctx->stream));
+    }
+};
+
 // Shared state of an in-process group: a generation barrier that any rank can
 // abort (a rank that throws must not leave the others waiting forever).
 struct ThreadGroup {

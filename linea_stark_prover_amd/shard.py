@@ -45,6 +45,10 @@ class GlooComm:
         self.dist, self.group = dist, group
         self.rank, self.size = dist.get_rank(group), dist.get_world_size(group)
         self.error: Optional[BaseException] = None
+        # every collective the library issued through this communicator, in
+        # order: (op, bytes per rank, root) -- identical on every rank, or a
+        # collective transport (RCCL) would deadlock (tests/test_gpu_shard_mp.py)
+        self.schedule = []
         self._ag = L.ALLGATHER_FN(self._allgather)
         self._bc = L.BCAST_FN(self._bcast)
         self.ops = L.LspCommOps(self.rank, self.size, None, self._ag, self._bc)
@@ -54,6 +58,7 @@ class GlooComm:
         return np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(ptr))
 
     def _allgather(self, _user, send, recv, nbytes):
+        self.schedule.append(("allgather", int(nbytes), None))
         try:
             src = torch.from_numpy(self._view(send, nbytes).copy())
             parts = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.size)]
@@ -67,6 +72,7 @@ class GlooComm:
             return 1
 
     def _bcast(self, _user, buf, nbytes, root):
+        self.schedule.append(("bcast", int(nbytes), int(root)))
         try:
             v = self._view(buf, nbytes)
             t = torch.from_numpy(v.copy())

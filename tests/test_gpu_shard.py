@@ -98,3 +98,45 @@ def test_group_large_equals_single(gpu_ctx):
     single = gpu_ctx.prove(tr, permutation_air(3), pub)
     grp, _ = _group(gpu_ctx, 8)
     assert grp.prove(tr, permutation_air(3), pub) == single
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_loopback_rank_rehearsal(product_lib, rank):
+    """tools/rank_rehearsal.py's transport: rank g of 8 proves its share at a
+    small size on its own (peers fabricated), returns a proof of the real
+    proof's shape, and reports its pool; the memory grows with the size"""
+    import ctypes
+    from linea_stark_prover_amd import _lib as L
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import Context, StarkConfig, _take_proof
+    cfg = StarkConfig()
+    a, d, _ = cfg.seeded()
+    pub = np.concatenate([a, d])
+    pools = []
+    for log_n in (12, 14):
+        with Context(cfg) as ctx:
+            L.check(L.lib().lsp_ctx_attach_loopback(ctx.h, rank, 8), ctx.h)
+            dt = ctx.gen_permutation_trace_device(log_n, 3, a, d)
+            desc = (ctypes.c_int32 * len(permutation_air(3).descriptor()))(*permutation_air(3).descriptor())
+            h = ctypes.c_void_p()
+            ctx._chk(L.lib().lsp_prove_sharded(ctx.h, dt, 1 << log_n, 8, desc, len(desc), pub.ctypes.data, 2,
+                                               L.LSP_MEM_DEVICE, ctypes.byref(h)))
+            proof = _take_proof(h)
+            ctx.dev_free(dt)
+            pool, used, tot = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+            ctx._chk(L.lib().lsp_ctx_mem_stats(ctx.h, ctypes.byref(pool), ctypes.byref(used), ctypes.byref(tot)))
+            assert 0 < pool.value <= used.value <= tot.value
+            pools.append(pool.value)
+            with Context(cfg) as ref:
+                real = ref.prove(ref_trace(ref, log_n, a, d), permutation_air(3), pub)
+            assert len(proof) == len(real)  # same shape, fabricated peer data
+    assert pools[1] > pools[0]
+
+
+def ref_trace(ctx, log_n, a, d):
+    h, w = 1 << log_n, 8
+    p = ctx.gen_permutation_trace_device(log_n, 3, a, d)
+    out = np.zeros((h, w, 4), np.uint64)
+    ctx.d2h(out, p)
+    ctx.dev_free(p)
+    return out

@@ -15,15 +15,20 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(tmp_path, nproc, comm, port, log_n=10):
-    out = tmp_path / f"proof_{comm}_{nproc}.bin"
+def _run(tmp_path, nproc, comm, port, log_n=10, schedules=None):
+    out = tmp_path / f"proof_{comm}_{nproc}_{log_n}.bin"
+    sched = tmp_path / f"sched_{nproc}_{log_n}"
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", LSP_FRI_SHARD_MIN="16")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
            "--gpus", str(nproc), "--shard", "--comm", comm, "--device", "0", "--log-n", str(log_n), "--steps", "1",
-           "--warmup", "0", "--no-cpu-baseline", "--dump-proof", str(out)]
+           "--warmup", "0", "--no-cpu-baseline", "--dump-proof", str(out), "--dump-comm-schedule", str(sched)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    if schedules is not None and comm == "gloo":
+        import json
+        for rk in range(nproc):
+            schedules.append(json.load(open(f"{sched}.{rk}.json")))
     return out.read_bytes()
 
 
@@ -41,6 +46,21 @@ def test_two_processes_gloo(gpu_ctx, tmp_path):
 
 def test_four_processes_gloo(gpu_ctx, tmp_path):
     assert _run(tmp_path, 4, "gloo", 29612) == _single(gpu_ctx)
+
+
+@pytest.mark.parametrize("log_n", [10, 12])
+def test_eight_processes_gloo(gpu_ctx, tmp_path, log_n):
+    """BASELINE configs[3]'s rank count (8 processes, here all on the box's one
+    GPU over gloo): the proof equals the single-GPU proof byte for byte, and
+    every rank issued the same collectives in the same order with the same
+    sizes and roots -- what a collective transport (RCCL) needs not to hang."""
+    scheds = []
+    assert _run(tmp_path, 8, "gloo", 29614 + log_n, log_n, scheds) == _single(gpu_ctx, log_n)
+    assert [s["rank"] for s in scheds] == list(range(8)) and all(s["world"] == 8 for s in scheds)
+    ref = scheds[0]["schedule"]
+    assert len(ref) >= 5 and {op for op, _, _ in ref} == {"allgather", "bcast"}
+    for s in scheds[1:]:
+        assert s["schedule"] == ref, f"rank {s['rank']} issued a different collective schedule"
 
 
 def test_rccl_transport_single_rank(gpu_ctx, tmp_path):

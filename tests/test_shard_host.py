@@ -27,7 +27,8 @@ WORKER = textwrap.dedent("""
     rc1 = c.ops.allgather(None, mine.ctypes.data, recv.ctypes.data, n)
     buf = mine.copy() if c.rank == 1 else np.zeros(n, np.uint8)
     rc2 = c.ops.bcast(None, buf.ctypes.data, n, 1)
-    print(json.dumps({{"rank": c.rank, "rc": [rc1, rc2], "recv": recv.tolist(), "bcast": buf.tolist()}}), flush=True)
+    print(json.dumps({{"rank": c.rank, "rc": [rc1, rc2], "recv": recv.tolist(), "bcast": buf.tolist(),
+                      "schedule": c.schedule}}), flush=True)
     d.close()
 """)
 
@@ -63,6 +64,9 @@ def test_gloo_comm_ops_two_ranks(tmp_path, product_lib):
         assert o["rc"] == [0, 0]
         assert o["recv"] == exp
         assert o["bcast"] == exp[n:]  # rank 1's pattern on every rank
+        # the communicator records what it carried, in order (the 8-process GPU
+        # test compares these schedules across ranks)
+        assert o["schedule"] == [["allgather", n, None], ["bcast", n, 1]]
 
 
 @pytest.fixture
@@ -99,3 +103,18 @@ def test_group_needs_gpu_contexts(host_ctx):
     from linea_stark_prover_amd.prover import ProverGroup
     with pytest.raises(_lib.LspError, match="GPU context"):
         ProverGroup([host_ctx, host_ctx])
+
+
+def test_loopback_attach_and_mem_stats_checks(host_ctx):
+    """the rehearsal transport (lsp_ctx_attach_loopback) takes any rank of any
+    size without a peer; memory stats need the GPU a host-only context lacks"""
+    import ctypes
+    from linea_stark_prover_amd import _lib as L
+    assert L.lib().lsp_ctx_attach_loopback(host_ctx.h, 8, 8) == L.LSP_E_ARG
+    assert L.lib().lsp_ctx_attach_loopback(host_ctx.h, 7, 8) == L.LSP_OK
+    r, n = ctypes.c_int(), ctypes.c_int()
+    assert L.lib().lsp_comm_info(host_ctx.h, ctypes.byref(r), ctypes.byref(n)) == L.LSP_OK
+    assert (r.value, n.value) == (7, 8)
+    a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    assert L.lib().lsp_ctx_mem_stats(host_ctx.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)) == L.LSP_E_STATE
+    assert L.lib().lsp_ctx_detach_comm(host_ctx.h) == L.LSP_OK

@@ -27,6 +27,9 @@ namespace lsp {
 struct Comm {
     int rank = 0, size = 1;
     virtual ~Comm() {}
+    // LoopbackComm: peers' data is fabricated, so the proof's self-checks
+    // (the FRI final polynomial's degree) cannot hold and are skipped
+    virtual bool rehearsal() const { return false; }
     // recv[r * bytes ...] = rank r's send (device buffers, ordered on ctx->stream)
     virtual void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) = 0;
     // every rank's buf = root's buf (device buffer)
@@ -74,6 +77,7 @@ struct LoopbackComm : Comm {
     void bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) override {
         if (root != rank) LSP_HIP(hipMemsetAsync(buf, 0, bytes, ctx->stream));
     }
+    bool rehearsal() const override { return true; }
 };
 
 // Shared state of an in-process group: a generation barrier that any rank can

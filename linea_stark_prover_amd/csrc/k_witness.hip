@@ -2,20 +2,26 @@
 // RawPermutationTrace::get_trace (trace/src/permutation.rs:24-93) and
 // RawLookupTrace::get_trace (trace/src/lookup.rs:46-176), writing the
 // columns straight into the row-major trace of RawTrace::get_trace
-// (trace/src/lib.rs:94-106).
+// (trace/src/lib.rs:94-106).  Every kernel here is hand-written:
 //
 //   rows         one thread per row: copy the raw columns into the trace row,
 //                Horner row combinations sum_j c_j alpha^(k-1-j)
 //   inverses     launch_batch_inverse (k_field.hip)
-//   scans        the permutation check column is a prefix PRODUCT, the LogUp
-//                column a prefix SUM: hipCUB decoupled-lookback scans over Fr
-//   multiplicity LogUp's occurrence map (a HashMap keyed by the A row
-//                combination, entries consumed by the first enabled B row with
-//                the same key, row-major over (row, table)) as a stable LSD
-//                radix sort of every entry on (key, tag, position): in each
-//                run of equal keys the enabled A entries come first, so the
-//                first enabled B entry of the run receives the run's A count.
-#include <hipcub/hipcub.hpp>
+//   scans        the permutation check column is a prefix PRODUCT
+//                (trace/src/permutation.rs:72), the LogUp column a prefix SUM
+//                (trace/src/lookup.rs:152-160): a reduce-then-scan over
+//                2048-element tiles (tile aggregates up, their scan, then each
+//                tile rescanned from its prefix), recursive over the aggregates
+//   multiplicity LogUp's occurrence map (trace/src/lookup.rs:78-100,145-155: a
+//                HashMap keyed by the A row combination, counted over the
+//                enabled A rows, each entry consumed by the first enabled B
+//                entry with the same key in (row, table) order) as a device
+//                hash table keyed by the combination: enabled A rows add 1 to
+//                their key's count, enabled B entries atomicMin their (row,
+//                table) position into it; the B entry holding the minimum
+//                receives the count.  Sums and minima do not depend on the
+//                order the threads run in, so the result is deterministic.
+#include <algorithm>
 
 #include "k_common.hpp"
 #include "kernels.hpp"
@@ -23,12 +29,93 @@
 namespace lsp {
 
 namespace {
+// the scan operators (both commutative and associative in Fr)
 struct FrMulOp {
     __device__ Fr operator()(const Fr& a, const Fr& b) const { return fr_mul(a, b); }
+    __device__ static Fr identity() { return fr_one(); }
 };
 struct FrAddOp {
     __device__ Fr operator()(const Fr& a, const Fr& b) const { return fr_add(a, b); }
+    __device__ static Fr identity() { return fr_zero(); }
 };
+
+// ---- inclusive scan: tiles of SC_PER contiguous elements per thread
+constexpr uint32_t SC_THREADS = 256, SC_PER = 8, SC_TILE = SC_THREADS * SC_PER;
+
+// this thread's SC_PER elements of the tile, folded
+template <class Op>
+__device__ __forceinline__ Fr sc_thread_agg(const Fr* __restrict__ in, size_t n, size_t base, Op op) {
+    Fr a = Op::identity();
+#pragma unroll
+    for (uint32_t j = 0; j < SC_PER; ++j)
+        if (base + j < n) a = op(a, in[base + j]);
+    return a;
+}
+
+// exclusive scan of the block's thread values (Hillis-Steele in LDS); *total = all of them
+template <class Op>
+__device__ __forceinline__ Fr sc_block_excl(Fr v, Fr* lds, Op op, Fr* total) {
+    const uint32_t t = threadIdx.x;
+    lds[t] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < SC_THREADS; d <<= 1) {
+        const Fr x = t >= d ? op(lds[t - d], v) : v;
+        __syncthreads();
+        lds[t] = x;
+        v = x;
+        __syncthreads();
+    }
+    const Fr ex = t ? lds[t - 1] : Op::identity();
+    if (total) *total = lds[SC_THREADS - 1];
+    return ex;
+}
+
+template <class Op>
+__global__ __launch_bounds__(SC_THREADS) void k_scan_up(const Fr* __restrict__ in, size_t n, Fr* __restrict__ agg) {
+    __shared__ Fr lds[SC_THREADS];
+    const Op op;
+    const size_t base = (size_t)blockIdx.x * SC_TILE + (size_t)threadIdx.x * SC_PER;
+    Fr total;
+    sc_block_excl(sc_thread_agg(in, n, base, op), lds, op, &total);
+    if (threadIdx.x == 0) agg[blockIdx.x] = total;
+}
+
+// incl_agg (nullable): the inclusive scan of the tile aggregates; tile b starts from incl_agg[b - 1]
+template <class Op>
+__global__ __launch_bounds__(SC_THREADS) void k_scan_down(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n,
+                                                          const Fr* __restrict__ incl_agg) {
+    __shared__ Fr lds[SC_THREADS];
+    const Op op;
+    const size_t base = (size_t)blockIdx.x * SC_TILE + (size_t)threadIdx.x * SC_PER;
+    Fr pre = sc_block_excl(sc_thread_agg(in, n, base, op), lds, op, nullptr);
+    if (incl_agg && blockIdx.x) pre = op(incl_agg[blockIdx.x - 1], pre);
+#pragma unroll
+    for (uint32_t j = 0; j < SC_PER; ++j) {
+        if (base + j >= n) break;
+        pre = op(pre, in[base + j]);
+        out[base + j] = pre;
+    }
+}
+
+template <class Op>
+hipError_t scan_rec(const Fr* in, Fr* out, size_t n, Fr* scratch, size_t cap, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const size_t T = (n + SC_TILE - 1) / SC_TILE;
+    if (T == 1) {
+        hipLaunchKernelGGL(k_scan_down<Op>, dim3(1), dim3(SC_THREADS), 0, st, in, out, n, nullptr);
+        return hipGetLastError();
+    }
+    if (2 * T > cap) return hipErrorInvalidValue;
+    Fr* agg = scratch;
+    Fr* agg_incl = scratch + T;
+    hipLaunchKernelGGL(k_scan_up<Op>, dim3((unsigned)T), dim3(SC_THREADS), 0, st, in, n, agg);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = scan_rec<Op>(agg, agg_incl, T, scratch + 2 * T, cap - 2 * T, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_scan_down<Op>, dim3((unsigned)T), dim3(SC_THREADS), 0, st, in, out, n, agg_incl);
+    return hipGetLastError();
+}
 
 __device__ __forceinline__ bool fr_nonzero(const Fr& x) {
     uint32_t o = 0;
@@ -91,57 +178,68 @@ __global__ __launch_bounds__(256) void k_lookup_rows(const Fr* __restrict__ a, u
     for (uint32_t t = 0; t < nt; ++t) row[f0 + 1 + t] = bfil[(size_t)t * n + i];
 }
 
-// sort record r: r < n -> A row r; else B entry (t, i) = ((r-n)/n, (r-n)%n).
-// tag 0 = enabled A, 1 = enabled B, 2 = disabled (sorts after both)
-__device__ __forceinline__ uint64_t rec_tagpos(uint32_t r, size_t n, uint32_t nt, const Fr* afil, const Fr* bfil) {
-    if (r < n) return (fr_nonzero(afil[r]) ? 0ull : 2ull) << 40 | r;
-    const size_t t = (r - n) / n, i = (r - n) % n;
-    const uint64_t tag = fr_nonzero(bfil[t * n + i]) ? 1ull : 2ull;
-    return tag << 40 | (i * nt + t);
+// ---- LogUp occurrences: a device hash table over the row combinations.
+// Record r: r < n -> A row r, key comb[r]; else B entry (t, i) with
+// r = n + t n + i, key comb[r] (comb is [A | table 0 | table 1 | ...]).
+constexpr uint32_t H_EMPTY = 0xffffffffu;
+
+__device__ __forceinline__ uint32_t key_hash(const Fr& k) {
+    uint64_t x = ((uint64_t)k.v[1] << 32 | k.v[0]) ^ (((uint64_t)k.v[5] << 32 | k.v[4]) * 0x9E3779B97F4A7C15ull);
+    x ^= x >> 29;
+    x *= 0xBF58476D1CE4E5B9ull;
+    return (uint32_t)(x ^ (x >> 32));
 }
 
-// pass 0: tag/position; pass 1..4: 64-bit word (pass-1) of the key
-__global__ __launch_bounds__(256) void k_sort_keys(const uint32_t* __restrict__ perm, size_t m, int pass,
-                                                   const Fr* __restrict__ comb, size_t n, uint32_t nt,
-                                                   const Fr* __restrict__ afil, const Fr* __restrict__ bfil,
-                                                   uint64_t* __restrict__ keys) {
-    const size_t j = gtid();
-    if (j >= m) return;
-    const uint32_t r = perm[j];
-    if (pass == 0) {
-        keys[j] = rec_tagpos(r, n, nt, afil, bfil);
-    } else {
-        const Fr& k = comb[r];
-        const int w = pass - 1;
-        keys[j] = (uint64_t)k.v[2 * w] | ((uint64_t)k.v[2 * w + 1] << 32);
+__device__ __forceinline__ bool rec_enabled(uint32_t r, size_t n, const Fr* afil, const Fr* bfil) {
+    return r < n ? fr_nonzero(afil[r]) : fr_nonzero(bfil[r - n]);
+}
+
+// the slot of comb[r]'s key (linear probing; insert claims an empty slot
+// with a CAS -- slots never change once claimed, so every thread with the
+// same key ends in the same slot).  Without insert the key must be present.
+__device__ __forceinline__ uint32_t occ_slot(const Fr* __restrict__ comb, uint32_t r, uint32_t* rep, uint32_t mask,
+                                             bool insert) {
+    const Fr key = comb[r];
+    uint32_t h = key_hash(key) & mask;
+    for (;;) {
+        uint32_t cur = __hip_atomic_load(rep + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == H_EMPTY && insert) {
+            cur = atomicCAS(rep + h, H_EMPTY, r);
+            if (cur == H_EMPTY) return h;
+        }
+        if (cur != H_EMPTY && (cur == r || fr_eq(comb[cur], key))) return h;
+        h = (h + 1) & mask;
     }
 }
 
-__global__ __launch_bounds__(256) void k_iota(uint32_t* __restrict__ p, size_t m) {
-    const size_t j = gtid();
-    if (j < m) p[j] = (uint32_t)j;
+// enabled A rows count their key; enabled B entries record their (row, table)
+// position i nt + t, the order the reference's loop meets them in
+__global__ __launch_bounds__(256) void k_occ_insert(const Fr* __restrict__ comb, size_t n, uint32_t nt,
+                                                    const Fr* __restrict__ afil, const Fr* __restrict__ bfil, size_t m,
+                                                    uint32_t* rep, uint32_t* cnt, unsigned long long* minb,
+                                                    uint32_t mask) {
+    const size_t r = gtid();
+    if (r >= m || !rec_enabled((uint32_t)r, n, afil, bfil)) return;
+    const uint32_t h = occ_slot(comb, (uint32_t)r, rep, mask, true);
+    if (r < n) {
+        atomicAdd(cnt + h, 1u);
+    } else {
+        const size_t t = (r - n) / n, i = (r - n) - t * n;
+        atomicMin(minb + h, (unsigned long long)(i * nt + t));
+    }
 }
 
-// run_start[j] = j if sorted record j starts a run of equal keys, else 0
-__global__ __launch_bounds__(256) void k_run_starts(const uint32_t* __restrict__ perm, size_t m,
-                                                    const Fr* __restrict__ comb, uint64_t* __restrict__ rs) {
-    const size_t j = gtid();
-    if (j >= m) return;
-    rs[j] = (j == 0 || !fr_eq(comb[perm[j]], comb[perm[j - 1]])) ? j : 0;
-}
-
-// the first enabled B entry of each run gets the run's count of enabled A entries
-__global__ __launch_bounds__(256) void k_first_b(const uint32_t* __restrict__ perm, size_t m, const uint64_t* rs,
-                                                 size_t n, uint32_t nt, const Fr* __restrict__ afil,
-                                                 const Fr* __restrict__ bfil, uint32_t* __restrict__ occ) {
-    const size_t j = gtid();
-    if (j >= m) return;
-    const uint32_t r = perm[j];
-    if ((rec_tagpos(r, n, nt, afil, bfil) >> 40) != 1) return;
-    const size_t s = rs[j];
-    if (j != s && (rec_tagpos(perm[j - 1], n, nt, afil, bfil) >> 40) == 1) return;  // not the first B of its run
-    // records s .. j-1 of the run are its enabled A entries (tag 0 sorts first)
-    occ[r - n] = (uint32_t)(j - s);
+// the first enabled B entry of each key takes the key's count of enabled A rows
+__global__ __launch_bounds__(256) void k_occ_assign(const Fr* __restrict__ comb, size_t n, uint32_t nt,
+                                                    const Fr* __restrict__ bfil, uint32_t* rep,
+                                                    const uint32_t* __restrict__ cnt,
+                                                    const unsigned long long* __restrict__ minb, uint32_t mask,
+                                                    uint32_t* __restrict__ occ) {
+    const size_t j = gtid();  // B entry t n + i
+    if (j >= n * nt || !fr_nonzero(bfil[j])) return;
+    const uint32_t h = occ_slot(comb, (uint32_t)(n + j), rep, mask, false);
+    const size_t t = j / n, i = j - t * n;
+    if (minb[h] == (unsigned long long)(i * nt + t)) occ[j] = cnt[h];
 }
 
 // term[i] = [a_filter != 0] a_inv[i] - sum_t occ[t][i] b_inv[t][i]; writes the
@@ -176,20 +274,6 @@ __global__ __launch_bounds__(256) void k_put_col(const Fr* __restrict__ v, size_
                                                  size_t ostride, uint32_t col) {
     const size_t i = gtid();
     if (i < n) out[i * ostride + col] = v[i];
-}
-
-// hipCUB temp storage in a caller scratch region
-struct Scratch {
-    void* p;
-    size_t cap;
-};
-template <class F>
-hipError_t with_temp(Scratch s, F&& f) {
-    size_t need = 0;
-    hipError_t e = f(nullptr, need);
-    if (e != hipSuccess) return e;
-    if (need > s.cap) return hipErrorInvalidValue;
-    return f(s.p, need);
 }
 
 // Synthetic raw permutation columns generated on the device (bench inputs at
@@ -228,10 +312,20 @@ __global__ __launch_bounds__(256) void k_gen_raw_perm(uint64_t seed, size_t n, u
 }
 }  // namespace
 
+// the occurrence table's capacity: a power of two >= 2 records (load <= 1/2)
+static size_t occ_capacity(size_t m) {
+    size_t c = 64;
+    while (c < 2 * m) c <<= 1;
+    return c;
+}
+
 size_t witness_scratch_bytes(size_t n, uint32_t nt) {
-    // sort keys/perms (double buffered) + run starts + hipCUB temp (generous bound)
+    // the occurrence table (4 + 4 + 8 bytes per slot) or the scans' tile
+    // aggregates (2 per tile, every level), whichever a block needs
     const size_t m = n * (1 + (size_t)nt);
-    return m * (2 * sizeof(uint64_t) + 2 * sizeof(uint32_t) + 2 * sizeof(uint64_t)) + 6 * 256 + (64u << 20) + m * 64;
+    const size_t table = occ_capacity(m) * 16 + 3 * 256;
+    const size_t scan = (2 * (n / SC_TILE + 1) + 64) * sizeof(Fr) * 2;
+    return std::max(table, scan);
 }
 
 hipError_t launch_gen_raw_perm(uint64_t seed, size_t n, uint32_t ncols, uint64_t mul, uint64_t add, Fr* a, Fr* b,
@@ -267,56 +361,32 @@ hipError_t launch_put_col(const Fr* v, size_t n, Fr* out, size_t ostride, uint32
 
 hipError_t launch_fr_scan(const Fr* in, Fr* out, size_t n, bool product, void* scratch, size_t scratch_bytes,
                           hipStream_t st) {
-    Scratch s{scratch, scratch_bytes};
-    if (product)
-        return with_temp(s, [&](void* p, size_t& b) {
-            return hipcub::DeviceScan::InclusiveScan(p, b, in, out, FrMulOp(), (int)n, st);
-        });
-    return with_temp(s, [&](void* p, size_t& b) {
-        return hipcub::DeviceScan::InclusiveScan(p, b, in, out, FrAddOp(), (int)n, st);
-    });
+    Fr* s = (Fr*)scratch;
+    const size_t cap = scratch_bytes / sizeof(Fr);
+    return product ? scan_rec<FrMulOp>(in, out, n, s, cap, st) : scan_rec<FrAddOp>(in, out, n, s, cap, st);
 }
 
 hipError_t launch_lookup_occurrences(const Fr* comb, size_t n, uint32_t nt, const Fr* afil, const Fr* bfil,
                                      uint32_t* occ, void* scratch, size_t scratch_bytes, hipStream_t st) {
     const size_t m = n * (1 + (size_t)nt);
-    // every partition 256-byte aligned (hipCUB's temp storage expects it)
+    if (m >= H_EMPTY) return hipErrorInvalidValue;  // record ids are 32-bit
+    const size_t cap = occ_capacity(m);
     char* p = (char*)scratch;
-    size_t off = 0;
-    auto carve = [&](size_t bytes) {
-        char* q = p + off;
-        off += (bytes + 255) & ~(size_t)255;
-        return q;
-    };
-    uint64_t* k0 = (uint64_t*)carve(m * 8);
-    uint64_t* k1 = (uint64_t*)carve(m * 8);
-    uint32_t* p0 = (uint32_t*)carve(m * 4);
-    uint32_t* p1 = (uint32_t*)carve(m * 4);
-    uint64_t* rs = (uint64_t*)carve(m * 8);
-    uint64_t* rs2 = (uint64_t*)carve(m * 8);
-    char* tmp = p + off;
-    const size_t used = off;
-    if (used > scratch_bytes) return hipErrorInvalidValue;
-    Scratch s{tmp, scratch_bytes - used};
-    const unsigned g = nblocks(m, 256);
-    hipLaunchKernelGGL(k_iota, dim3(g), dim3(256), 0, st, p0, m);
-    for (int pass = 0; pass < 5; ++pass) {
-        hipLaunchKernelGGL(k_sort_keys, dim3(g), dim3(256), 0, st, p0, m, pass, comb, n, nt, afil, bfil, k0);
-        const int end_bit = pass == 0 ? 42 : 64;
-        hipError_t e = with_temp(s, [&](void* t, size_t& b) {
-            return hipcub::DeviceRadixSort::SortPairs(t, b, k0, k1, p0, p1, (int)m, 0, end_bit, st);
-        });
-        if (e != hipSuccess) return e;
-        std::swap(p0, p1);
-    }
-    hipLaunchKernelGGL(k_run_starts, dim3(g), dim3(256), 0, st, p0, m, comb, rs);
-    hipError_t e = with_temp(s, [&](void* t, size_t& b) {
-        return hipcub::DeviceScan::InclusiveScan(t, b, rs, rs2, hipcub::Max(), (int)m, st);
-    });
+    auto* minb = (unsigned long long*)p;  // 8-byte entries first (alignment)
+    auto* rep = (uint32_t*)(p + cap * 8);
+    auto* cnt = rep + cap;
+    if (cap * 16 > scratch_bytes) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(minb, 0xff, cap * 8, st);
+    if (e == hipSuccess) e = hipMemsetAsync(rep, 0xff, cap * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, cap * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(occ, 0, n * nt * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    e = hipMemsetAsync(occ, 0, n * nt * sizeof(uint32_t), st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_first_b, dim3(g), dim3(256), 0, st, p0, m, rs2, n, nt, afil, bfil, occ);
+    const uint32_t mask = (uint32_t)(cap - 1);
+    hipLaunchKernelGGL(k_occ_insert, dim3(nblocks(m, 256)), dim3(256), 0, st, comb, n, nt, afil, bfil, m, rep, cnt,
+                       minb, mask);
+    if (nt)
+        hipLaunchKernelGGL(k_occ_assign, dim3(nblocks(n * nt, 256)), dim3(256), 0, st, comb, n, nt, bfil, rep, cnt, minb,
+                           mask, occ);
     return hipGetLastError();
 }
 

@@ -39,6 +39,8 @@ enum PassMode : int { PASS_INPLACE = 0, PASS_INV_FIRST = 1, PASS_INV_FWD = 2 };
 
 struct NttPass {
     const Fr* src;      // PASS_INV_FIRST: caller rows; PASS_INV_FWD: X after the earlier inverse passes (or caller rows)
+    ColMap src_map;     // where column c of the transform sits in src (PASS_INV_FIRST, PASS_INV_FWD)
+    uint32_t no_inv;    // PASS_INV_FWD: src holds the coefficients already (no inverse stages; launch_lde_coeffs)
     Fr* dst;            // the arrays being transformed (h rows each, batch of `narr` arrays, row-major w)
     const uint4* tw;    // stage-major twiddles (launch_stage_twiddles), 29-bit limbs, 3 x uint4 per element
     const uint4* tw_inv;  // PASS_INV_FWD: the inverse transform's twiddles
@@ -53,6 +55,20 @@ struct NttPass {
     uint32_t twl_n;     // PASS_INV_FWD: forward twiddles cached in LDS (G (2^k - 1) entries; 0: read from tw)
     uint64_t narr;      // arrays (cosets) in dst
 };
+
+// element (row, col) of a pass's source through its column map; false: a
+// padding column (reads as zero)
+__device__ __forceinline__ bool src_at(const ColMap& m, uint64_t H, uint32_t row, uint32_t col, size_t& idx) {
+    if (m.logb == COLMAP_PLAIN) {
+        const uint32_t sc = m.c0 + m.cstep * col;
+        if (sc >= m.valid) return false;
+        idx = (size_t)row * m.stride + sc;
+        return true;
+    }
+    const uint32_t b = brev_bits(col & ((1u << m.logb) - 1), m.logb), c = col >> m.logb;
+    idx = ((size_t)b * H + row) * m.bw + c;
+    return true;
+}
 
 // x^i from a two-level table of 29-bit-form factors: the product of two
 // 29-bit-form values is the 29-bit form of the product
@@ -385,10 +401,11 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
             if (c >= cw) continue;
             const uint32_t row = gm.row_of(t, g);
             const uint32_t srow = p.inv_gather ? brev_bits(row, p.logH) : row;
-            T.put(gm.idx(t, g, c), f29_repack_in(p.src[(size_t)srow * p.w + c0 + c]));
+            size_t si;
+            T.put(gm.idx(t, g, c), src_at(p.src_map, H, srow, c0 + c, si) ? f29_repack_in(p.src[si]) : f29_zero());
         }
         __syncthreads();
-        tile_stages<false, LOGCW>(T, gm, p.tw_inv, p.logH - p.k, p.logH, n_el);
+        if (!p.no_inv) tile_stages<false, LOGCW>(T, gm, p.tw_inv, p.logH - p.k, p.logH, n_el);
 #pragma unroll
         for (uint32_t j = 0; j < NREG; ++j) {
             const uint32_t e = threadIdx.x + j * NTT_THREADS;
@@ -436,8 +453,9 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
                 if (c >= cw) continue;
                 const uint32_t row = gm.row_of(t, g);
                 F29 v;
+                size_t si;
                 if (MODE == PASS_INV_FIRST)
-                    v = f29_repack_in(p.src[(size_t)brev_bits(row, p.logH) * p.w + c0 + c]);
+                    v = src_at(p.src_map, H, brev_bits(row, p.logH), c0 + c, si) ? f29_repack_in(p.src[si]) : f29_zero();
                 else
                     v = f29_repack_in(base[(size_t)row * p.w + c0 + c]);
                 T.put(gm.idx(t, g, c), v);
@@ -518,9 +536,14 @@ void plan_passes(uint32_t logH, uint32_t kmax, uint32_t* ks, uint32_t& np) {
 }
 }  // namespace
 
-hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t ncosets, const uint4* tw_inv,
-                      const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
-                      hipStream_t st) {
+// the passes of an LDE (WHAT = LDE_FULL), of its inverse half only
+// (LDE_INV: X <- h * coefficients) or of its forward half only (LDE_FWD: from
+// h * coefficients at `in` through `map`)
+enum LdeWhat { LDE_FULL = 0, LDE_INV = 1, LDE_FWD = 2 };
+
+static hipError_t run_lde(LdeWhat what, const Fr* in, ColMap map, Fr* X, Fr* out, size_t w, uint32_t logh,
+                          uint32_t ncosets, const uint4* tw_inv, const uint4* tw_fwd, const Fr* twist, uint32_t L1,
+                          uint32_t L2, int twist_per_col, hipStream_t st) {
     if (w == 0) return hipSuccess;
     // Tile = 2^k positions x G groups x CW columns = 1024 elements (36 KiB of
     // LDS) where the array allows it, so every radix-4 group gives each of the
@@ -567,10 +590,12 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
         const uint32_t logG = std::min(logh - k, want);
         NttPass p;
         p.src = src;
+        p.src_map = map;  // read only by the passes with a `src` (PASS_INV_FIRST / PASS_INV_FWD)
+        p.no_inv = what == LDE_FWD ? 1u : 0u;
         p.dst = dst;
         p.tw = tw;
         p.tw_inv = tw_inv;
-        p.inv_gather = np == 1 ? 1u : 0u;
+        p.inv_gather = (np == 1 && what == LDE_FULL) ? 1u : 0u;
         p.twist = twist;
         p.L1 = L1;
         p.L2 = L2;
@@ -617,20 +642,33 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
     };
     if (logh == 0) {
         // h = 1: the coefficient is the value; every coset row equals it
+        if (what == LDE_INV || map.logb != COLMAP_PLAIN || map.c0 != 0 || map.cstep != 1 || map.stride != w)
+            return hipErrorInvalidValue;  // (the sharded prover's maps never meet h = 1)
         for (uint32_t k = 0; k < ncosets; ++k) {
             hipError_t e = hipMemcpyAsync(out + (size_t)k * w, in, w * sizeof(Fr), hipMemcpyDeviceToDevice, st);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
     }
-    uint32_t s0 = 0;
-    for (uint32_t q = 0; q + 1 < np; ++q) {  // inverse passes before the last
-        hipError_t e = launch(false, q == 0 ? PASS_INV_FIRST : PASS_INPLACE, ks[q], s0, 1, in, X, tw_inv, false);
-        if (e != hipSuccess) return e;
-        s0 += ks[q];
+    hipError_t e = hipSuccess;
+    if (what == LDE_INV) {  // every inverse pass, the last one too, into X
+        uint32_t s0 = 0;
+        for (uint32_t q = 0; q < np && e == hipSuccess; ++q) {
+            e = launch(false, q == 0 ? PASS_INV_FIRST : PASS_INPLACE, ks[q], s0, 1, in, X, tw_inv, false);
+            s0 += ks[q];
+        }
+        return e;
     }
-    // the inverse's last stages + the forward's first ks[np-1] stages, per coset
-    hipError_t e = launch(true, PASS_INV_FWD, ks[np - 1], 0, ncosets, np == 1 ? in : X, out, tw_fwd, np == 1);
+    uint32_t s0 = 0;
+    if (what == LDE_FULL)
+        for (uint32_t q = 0; q + 1 < np; ++q) {  // inverse passes before the last
+            e = launch(false, q == 0 ? PASS_INV_FIRST : PASS_INPLACE, ks[q], s0, 1, in, X, tw_inv, false);
+            if (e != hipSuccess) return e;
+            s0 += ks[q];
+        }
+    // the inverse's last stages (LDE_FULL) + the forward's first ks[np-1] stages, per coset
+    e = launch(true, PASS_INV_FWD, ks[np - 1], 0, ncosets, (np == 1 || what == LDE_FWD) ? in : X, out, tw_fwd,
+               np == 1);
     if (e != hipSuccess) return e;
     s0 = ks[np - 1];
     for (uint32_t q = 1; q < np; ++q) {  // the remaining forward passes
@@ -640,6 +678,24 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
         s0 += k;
     }
     return hipSuccess;
+}
+
+hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t ncosets, const uint4* tw_inv,
+                      const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
+                      hipStream_t st) {
+    return run_lde(LDE_FULL, in, ColMap::plain((uint32_t)w), X, out, w, logh, ncosets, tw_inv, tw_fwd, twist, L1, L2,
+                   twist_per_col, st);
+}
+
+hipError_t launch_intt(const Fr* in, ColMap map, Fr* X, size_t w, uint32_t logh, const uint4* tw_inv, hipStream_t st) {
+    return run_lde(LDE_INV, in, map, X, nullptr, w, logh, 0, tw_inv, nullptr, nullptr, 0, 0, 0, st);
+}
+
+hipError_t launch_lde_coeffs(const Fr* coef, ColMap map, Fr* out, size_t w, uint32_t logh, uint32_t ncosets,
+                             const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
+                             hipStream_t st) {
+    return run_lde(LDE_FWD, coef, map, nullptr, out, w, logh, ncosets, nullptr, tw_fwd, twist, L1, L2, twist_per_col,
+                   st);
 }
 
 hipError_t launch_to_f29form(const Fr* in, Fr* out, size_t n, hipStream_t st) {

@@ -12,6 +12,31 @@
 namespace lsp {
 
 // ------------------------------------------------------------ k_ntt.hip
+// Where column c of a transform sits in its source matrix.
+//   plain    element (row, c) at row * stride + c0 + cstep * c; source
+//            columns >= valid read as zero (a rank's strided column subset)
+//   blocked  the column-split layout of a sharded proof's coefficients: G =
+//            2^logb row-major blocks of h x bw, column c in block
+//            bitrev_logb(c mod G) at column c / G (rank g inverted the columns
+//            bitrev(g) + G k, and the blocks arrive in rank order)
+constexpr uint32_t COLMAP_PLAIN = 0xffu;
+struct ColMap {
+    uint32_t logb = COLMAP_PLAIN;
+    uint32_t stride = 0, c0 = 0, cstep = 1, valid = 0xffffffffu;
+    uint32_t bw = 0;
+    static ColMap plain(uint32_t w) {
+        ColMap m;
+        m.stride = w;
+        m.valid = w;
+        return m;
+    }
+    static ColMap blocked(uint32_t logb, uint32_t bw) {
+        ColMap m;
+        m.logb = logb;
+        m.bw = bw;
+        return m;
+    }
+};
 // Coset evaluations of the h x w row-major matrix `in`: `ncosets` blocks of h
 // rows (block k on the coset of twist table k), each in bit-reversed order,
 // into row-major `out` (canonical), via X (h x w scratch, left holding
@@ -22,6 +47,16 @@ namespace lsp {
 hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t ncosets, const uint4* tw_inv,
                       const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
                       hipStream_t st);
+// The two halves of launch_lde, for a sharded proof whose ranks split the
+// inverse transform by columns (prove.cpp prove_shard):
+//   launch_intt       X (h x w) <- h * coefficients, natural order, of the w
+//                     columns `map` picks in `in` (values on H_h)
+//   launch_lde_coeffs the coset blocks of launch_lde from h * coefficients at
+//                     `coef` through `map` (no inverse stages)
+hipError_t launch_intt(const Fr* in, ColMap map, Fr* X, size_t w, uint32_t logh, const uint4* tw_inv, hipStream_t st);
+hipError_t launch_lde_coeffs(const Fr* coef, ColMap map, Fr* out, size_t w, uint32_t logh, uint32_t ncosets,
+                             const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
+                             hipStream_t st);
 // ark-form words -> the 29-bit Montgomery form (x 2^261 mod r), canonical, in place allowed
 hipError_t launch_to_f29form(const Fr* in, Fr* out, size_t n, hipStream_t st);
 // the same, unpacked into 9 x 29-bit limbs padded to 48 bytes (3 x uint4 per

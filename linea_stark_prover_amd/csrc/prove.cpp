@@ -116,6 +116,55 @@ Fr d2h_fr(lsp_ctx* ctx, const Fr* d) {
 }  // namespace
 
 // ----------------------------------------------------------------- LDE
+// The twist tables of coset blocks [k0, k0 + nk) of an h x w LDE: coset k,
+// column c has base s = shift_c * w_N^bitrev(k); coefficient i is scaled by
+// s^i / h.  Built once per (log h, cosets, shifts) and kept in the context.
+struct TwistTables {
+    const Fr* tabs;
+    uint32_t L1, L2;
+    bool shared;  // one table per coset (every column's shift is the same)
+};
+static TwistTables lde_twist(lsp_ctx* ctx, size_t h, size_t w, uint32_t added_bits, const Fr* shifts_host, uint32_t k0,
+                             uint32_t nk) {
+    const uint32_t logh = log2_exact(h);
+    const uint32_t logN = logh + added_bits;
+    hipStream_t st = ctx->stream;
+    TwistTables T;
+    T.shared = true;
+    for (size_t c = 1; c < w; ++c) T.shared = T.shared && fr_eq(shifts_host[c], shifts_host[0]);
+    const size_t per_coset = T.shared ? 1 : w;
+    two_level(logh, T.L1, T.L2);
+    const size_t per = (1ull << T.L1) + (1ull << T.L2);
+    const size_t nb = (size_t)nk * per_coset;
+    uint64_t hsh = 1469598103934665603ull;  // FNV-1a over the shifts' words
+    for (size_t c = 0; c < per_coset; ++c)
+        for (int i = 0; i < 8; ++i) hsh = (hsh ^ shifts_host[c].v[i]) * 1099511628211ull;
+    char key[112];
+    std::snprintf(key, sizeof key, "ldetw_%u_%u_%u_%u_%zu_%016llx", logh, added_bits, k0, nk, per_coset,
+                  (unsigned long long)hsh);
+    auto it = ctx->ptabs.find(key);
+    if (it != ctx->ptabs.end()) {
+        T.tabs = it->second;
+        return T;
+    }
+    const Fr wN = host_two_adic_generator(logN);
+    const Fr hinv = host_inv_cached(fr_from_u64(h));
+    std::vector<Fr> bases(2 * nb, hinv);  // nb bases, then nb scales (1/h)
+    for (uint32_t k = 0; k < nk; ++k) {
+        const Fr ck = fr_pow_u64(wN, host_bitrev(k0 + k, added_bits));
+        for (size_t c = 0; c < per_coset; ++c) bases[k * per_coset + c] = fr_mul(shifts_host[c], ck);
+    }
+    Fr* dbases = ctx->fbuf("lde_bases", 2 * nb);
+    ctx->h2d_async("lde_bases_h", dbases, bases.data(), bases.size() * sizeof(Fr));
+    const bool keep = ctx->ptabs.size() < 256;  // API callers with ever new shifts: a scratch table
+    Fr* t = ctx->fbuf(keep ? key : "lde_tabs", per * nb);
+    LSP_HIP(launch_pow_tables(dbases, nb, T.L1, T.L2, dbases + nb, t, st));
+    LSP_HIP(launch_to_f29form(t, t, per * nb, st));  // the NTT multiplies by 29-bit-form factors
+    if (keep) ctx->ptabs[key] = t;
+    T.tabs = t;
+    return T;
+}
+
 // Coset blocks [k0, k0 + nk) of the bit-reversed LDE (nk = 0: all
 // 2^added_bits): block k = rows k*h .. (k+1)*h - 1 of the full LDE, the
 // evaluations on shift_c * w_N^bitrev(k) * H_h.  d_out receives nk blocks.
@@ -125,49 +174,34 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
     const uint32_t B = 1u << added_bits;
     if (nk == 0) nk = B;
     LSP_REQUIRE(k0 + nk <= B, LSP_E_ARG, "coset range outside the LDE");
-    const uint32_t logN = logh + added_bits;
-    LSP_REQUIRE(logN <= 47, LSP_E_SIZE, "LDE larger than the 2-adic subgroup");
+    LSP_REQUIRE(logh + added_bits <= 47, LSP_E_SIZE, "LDE larger than the 2-adic subgroup");
     Fr* X = ctx->fbuf("lde_X", h * w);
-    hipStream_t st = ctx->stream;
-    // coset k, column c: base s = shift_c * w_N^bitrev_B(k); coefficient i is scaled by s^i / h
-    bool shared = true;
-    for (size_t c = 1; c < w; ++c) shared = shared && fr_eq(shifts_host[c], shifts_host[0]);
-    const size_t per_coset = shared ? 1 : w;
-    uint32_t L1, L2;
-    two_level(logh, L1, L2);
-    const size_t per = (1ull << L1) + (1ull << L2);
-    const size_t nb = (size_t)nk * per_coset;
-    // the twist tables depend on the shape and the shifts only: built once per
-    // (log h, cosets, shifts) and kept in the context (pool-owned)
-    uint64_t hsh = 1469598103934665603ull;  // FNV-1a over the shifts' words
-    for (size_t c = 0; c < per_coset; ++c)
-        for (int i = 0; i < 8; ++i) hsh = (hsh ^ shifts_host[c].v[i]) * 1099511628211ull;
-    char key[112];
-    std::snprintf(key, sizeof key, "ldetw_%u_%u_%u_%u_%zu_%016llx", logh, added_bits, k0, nk, per_coset,
-                  (unsigned long long)hsh);
-    const Fr* tabs;
-    auto it = ctx->ptabs.find(key);
-    if (it != ctx->ptabs.end()) {
-        tabs = it->second;
-    } else {
-        const Fr wN = host_two_adic_generator(logN);
-        const Fr hinv = host_inv_cached(fr_from_u64(h));
-        std::vector<Fr> bases(2 * nb, hinv);  // nb bases, then nb scales (1/h)
-        for (uint32_t k = 0; k < nk; ++k) {
-            const Fr ck = fr_pow_u64(wN, host_bitrev(k0 + k, added_bits));
-            for (size_t c = 0; c < per_coset; ++c) bases[k * per_coset + c] = fr_mul(shifts_host[c], ck);
-        }
-        Fr* dbases = ctx->fbuf("lde_bases", 2 * nb);
-        ctx->h2d_async("lde_bases_h", dbases, bases.data(), bases.size() * sizeof(Fr));
-        const bool keep = ctx->ptabs.size() < 256;  // API callers with ever new shifts: a scratch table
-        Fr* t = ctx->fbuf(keep ? key : "lde_tabs", per * nb);
-        LSP_HIP(launch_pow_tables(dbases, nb, L1, L2, dbases + nb, t, st));
-        LSP_HIP(launch_to_f29form(t, t, per * nb, st));  // the NTT multiplies by 29-bit-form factors
-        if (keep) ctx->ptabs[key] = t;
-        tabs = t;
-    }
-    LSP_HIP(launch_lde(d_in, X, d_out, w, logh, nk, ctx->twiddle29(logh, true), ctx->twiddle29(logh, false), tabs, L1,
-                       L2, shared ? 0 : 1, st));
+    const TwistTables T = lde_twist(ctx, h, w, added_bits, shifts_host, k0, nk);
+    LSP_HIP(launch_lde(d_in, X, d_out, w, logh, nk, ctx->twiddle29(logh, true), ctx->twiddle29(logh, false), T.tabs,
+                       T.L1, T.L2, T.shared ? 0 : 1, ctx->stream));
+}
+
+// The same blocks from h * coefficients (natural order) at `coef`, laid out
+// as `map` says -- the forward half, for ranks that split the inverse
+static void lde_coeffs_device(lsp_ctx* ctx, const Fr* coef, ColMap map, size_t h, size_t w, uint32_t added_bits,
+                              const Fr* shifts_host, Fr* d_out, uint32_t k0, uint32_t nk) {
+    const uint32_t logh = log2_exact(h);
+    LSP_REQUIRE(k0 + nk <= (1u << added_bits) && logh >= 1, LSP_E_ARG, "coset range outside the LDE");
+    const TwistTables T = lde_twist(ctx, h, w, added_bits, shifts_host, k0, nk);
+    LSP_HIP(launch_lde_coeffs(coef, map, d_out, w, logh, nk, ctx->twiddle29(logh, false), T.tabs, T.L1, T.L2,
+                              T.shared ? 0 : 1, ctx->stream));
+}
+
+// A sharded proof splits the inverse NTTs by columns (rank g inverts the
+// columns bitrev(g) + G k and the coefficients are exchanged) instead of every
+// rank inverting every column; LSP_SHARD_SPLIT_INTT=0 restores the redundant
+// per-rank inverse (A/B)
+static bool split_intt() {
+    static const bool on = [] {
+        const char* e = std::getenv("LSP_SHARD_SPLIT_INTT");
+        return !(e && *e == '0');
+    }();
+    return on;
 }
 
 // ------------------------------------------------------------- Merkle
@@ -560,7 +594,23 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         std::vector<Fr> shifts(std::max(w, q), GEN);
         T.begin("coset_lde_batch");
         span("coset_lde_batch", w, h, (int)lb);
-        lde_device(ctx, d_trace, h, w, lb, shifts.data(), lde, k0, nk);
+        const bool split = G > 1 && split_intt();
+        if (split) {
+            // rank g inverts the columns bitrev(g) + G k (k < cg; columns past w
+            // are zero padding), the ranks allgather the h x cg coefficient
+            // blocks, and each transforms its own cosets from them
+            const uint32_t cg = (uint32_t)((w + G - 1) / G);
+            Fr* xl = ctx->fbuf("t_coef_local", h * cg);
+            Fr* coef = ctx->fbuf("t_coef", h * cg * G);
+            ColMap m = ColMap::plain((uint32_t)w);
+            m.c0 = (uint32_t)host_bitrev(g, b);
+            m.cstep = G;
+            LSP_HIP(launch_intt(d_trace, m, xl, cg, log_h, ctx->twiddle29(log_h, true), st));
+            comm.allgather(ctx, xl, coef, h * cg * sizeof(Fr));
+            lde_coeffs_device(ctx, coef, ColMap::blocked(b, cg), h, w, lb, shifts.data(), lde, k0, nk);
+        } else {
+            lde_device(ctx, d_trace, h, w, lb, shifts.data(), lde, k0, nk);
+        }
         T.end("coset_lde_batch");
         Fr* tlay = ctx->fbuf("t_tree", 2 * S - 1);
         std::vector<std::vector<Fr>> ttop, qtop;
@@ -585,10 +635,12 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         const Fr* tabQ = pow_table(ctx, "tabQ", host_two_adic_generator(logQ), logQ, L1Q);
         const Fr wh = host_two_adic_generator(log_h);
         const Fr wh_inv = host_inv_cached(wh);
-        Fr* qv = ctx->fbuf("q_values", Q);  // the h x q chunk matrix, on every rank
-        // ranks g < Gq evaluate points straight into their slot of the exchange buffer
+        // G = 1: the h x q chunk matrix.  G > 1: ranks g < Gq evaluate points
+        // into their slot of the exchange buffer (split: into a local buffer,
+        // whose inverse NTT goes to the slot)
+        Fr* qv = G == 1 || !split ? ctx->fbuf("q_values", Q) : nullptr;
         Fr* stage = G == 1 ? nullptr : ctx->fbuf("q_stage", Sq * Gq);
-        Fr* qloc = G == 1 ? qv : (g < Gq ? stage + (size_t)g * Sq : nullptr);
+        Fr* qloc = G == 1 ? qv : (g < Gq ? (split ? ctx->fbuf("q_vals_local", Sq) : stage + (size_t)g * Sq) : nullptr);
         std::vector<Fr> zh(q), izh(q);
         if (row0 < Q) {
             const uint64_t i0 = host_bitrev(g, logGq);
@@ -646,9 +698,14 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         }
         if (G > 1) {
             // rank r < Gq holds chunks j = bitrev(r) + Gq c as an h x cpr matrix: one
-            // broadcast per holder (only the Gq holders send: Gq/G of an allgather's bytes)
+            // broadcast per holder (only the Gq holders send: Gq/G of an allgather's bytes).
+            // split: the holder sends its chunks' coefficients (its own inverse
+            // NTT), and no rank inverts the whole h x q matrix
+            if (split && g < Gq)
+                LSP_HIP(launch_intt(qloc, ColMap::plain((uint32_t)cpr), stage + (size_t)g * Sq, cpr, log_h,
+                                    ctx->twiddle29(log_h, true), st));
             for (uint32_t r = 0; r < Gq; ++r) comm.bcast(ctx, stage + (size_t)r * Sq, Sq * sizeof(Fr), (int)r);
-            LSP_HIP(launch_assemble_chunks(stage, logGq, cpr, h, qv, st));
+            if (!split) LSP_HIP(launch_assemble_chunks(stage, logGq, cpr, h, qv, st));
         }
         T.end("compute quotient polynomial");
 
@@ -665,7 +722,10 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         Fr* qlde = ctx->fbuf("q_lde", S * q);
         T.begin("coset_lde_batch (quotient)");
         for (size_t j = 0; j < q; ++j) span("coset_lde_batch", 1, h, (int)lb);  // one launch, q independent columns
-        lde_device(ctx, qv, h, q, lb, shifts.data(), qlde, k0, nk);
+        if (split)  // the chunk coefficients straight from the exchange buffer (column j in slot bitrev(j mod Gq))
+            lde_coeffs_device(ctx, stage, ColMap::blocked(logGq, (uint32_t)cpr), h, q, lb, shifts.data(), qlde, k0, nk);
+        else
+            lde_device(ctx, qv, h, q, lb, shifts.data(), qlde, k0, nk);
         T.end("coset_lde_batch (quotient)");
         Fr* qlay = ctx->fbuf("q_tree", 2 * S - 1);
         proof->qroot = shard_root(ctx, comm, commit_device(ctx, one_mat(qlde, (uint32_t)q), S, qlay), qtop);

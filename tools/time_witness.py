@@ -44,6 +44,8 @@ for _ in range(3):
     ctx.synchronize()
     ts.append(time.perf_counter() - t0)
 print(f"GPU witness (incl. raw-column uploads), 2^{log_n} rows, width {rt.width}: {min(ts) * 1e3:.1f} ms")
+if "--gpu-only" in sys.argv:
+    sys.exit(0)
 t0 = time.perf_counter()
 tr, air = gen_wide_trace(log_n, a, d)
 print(f"host C++ lsp_gen_wide_trace (random columns + witness), width {tr.shape[1]}: {(time.perf_counter() - t0) * 1e3:.1f} ms")

@@ -85,20 +85,21 @@ struct Reader {
 }  // namespace
 
 std::vector<uint8_t> serialize(const lsp_proof& p) {
-    size_t nfr = 3 + p.tl.size() + p.tn.size() + p.qc.size() + p.roots.size() + p.final_poly.size(), nu32 = 5;
+    size_t nfr = 3 + p.tl.size() + p.tn.size() + p.qc.size() + p.roots.size() + p.final_poly.size(), nu32 = 6;
     for (auto& q : p.queries) {
         nfr += q.trow.size() + q.tpath.size() + q.qrow.size() + q.qpath.size() + q.sib.size();
         for (auto& f : q.fpath) nfr += f.size();
         nu32 += 2 + q.sib.size();
     }
     std::vector<uint8_t> b(8 + 4 * nu32 + 32 * nfr);
-    std::memcpy(b.data(), "LSPPRF01", 8);
+    std::memcpy(b.data(), "LSPPRF02", 8);
     Writer w{b.data() + 8};
     w.u32(p.log_h);
     w.u32(p.log_q);
     w.u32(p.w);
     w.u32((uint32_t)p.queries.size());
     w.u32((uint32_t)p.roots.size());
+    w.u32((uint32_t)p.final_poly.size());
     w.fr(p.troot);
     w.fr(p.qroot);
     w.frs(p.tl);
@@ -124,50 +125,47 @@ std::vector<uint8_t> serialize(const lsp_proof& p) {
     return b;
 }
 
-// The wire format does not record the final polynomial's length: it is what
-// is left once every query is read, so the reader tries lengths 1, 2, 4, ...
-// (<= 2^20) and keeps the one that consumes the buffer exactly.
+// Untrusted bytes: every count is range-checked before anything is sized by
+// it, and the buffer must be consumed exactly.
 lsp_proof* deserialize(const uint8_t* buf, size_t len) {
-    if (!buf || len < 8 + 20 || std::memcmp(buf, "LSPPRF01", 8) != 0)
-        throw LspError(LSP_E_ARG, "not an LSPPRF01 proof");
-    for (uint32_t lf = 0; lf <= 20; ++lf) {
-        Reader r{buf, len};
-        r.off = 8;
-        auto p = std::make_unique<lsp_proof>();
-        p->log_h = r.u32();
-        p->log_q = r.u32();
-        p->w = r.u32();
-        const uint32_t nq = r.u32(), nr = r.u32();
-        if (r.bad || p->log_h > 40 || p->log_q > 20 || p->w == 0 || p->w > (1u << 20) || nr > 64 || nq > (1u << 20))
-            throw LspError(LSP_E_ARG, "proof header out of range");
-        const size_t q = (size_t)1 << p->log_q;
-        p->troot = r.fr();
-        p->qroot = r.fr();
-        r.frs(p->tl, p->w);
-        r.frs(p->tn, p->w);
-        r.frs(p->qc, q);
-        r.frs(p->roots, nr);
-        r.frs(p->final_poly, (size_t)1 << lf);
-        p->pow_w = r.fr();
-        if (r.bad) break;  // longer final polynomials cannot fit either
-        if (nq > (len - r.off) / (32 * (p->w + q))) break;
-        p->queries.resize(nq);
-        for (auto& qq : p->queries) {
-            r.frs(qq.trow, p->w);
-            r.frs(qq.tpath, r.u32());
-            r.frs(qq.qrow, q);
-            r.frs(qq.qpath, r.u32());
-            qq.sib.resize(nr);
-            qq.fpath.resize(nr);
-            for (uint32_t k = 0; k < nr && !r.bad; ++k) {
-                qq.sib[k] = r.fr();
-                r.frs(qq.fpath[k], r.u32());
-            }
-            if (r.bad) break;
+    if (!buf || len < 8 + 24 || std::memcmp(buf, "LSPPRF02", 8) != 0)
+        throw LspError(LSP_E_ARG, "not an LSPPRF02 proof");
+    Reader r{buf, len};
+    r.off = 8;
+    auto p = std::make_unique<lsp_proof>();
+    p->log_h = r.u32();
+    p->log_q = r.u32();
+    p->w = r.u32();
+    const uint32_t nq = r.u32(), nr = r.u32(), nf = r.u32();
+    if (r.bad || p->log_h > 40 || p->log_q > 20 || p->w == 0 || p->w > (1u << 20) || nr > 64 || nq > (1u << 20) ||
+        nf == 0 || nf > (1u << 20) || (nf & (nf - 1)) != 0)
+        throw LspError(LSP_E_ARG, "proof header out of range");
+    const size_t q = (size_t)1 << p->log_q;
+    p->troot = r.fr();
+    p->qroot = r.fr();
+    r.frs(p->tl, p->w);
+    r.frs(p->tn, p->w);
+    r.frs(p->qc, q);
+    r.frs(p->roots, nr);
+    r.frs(p->final_poly, nf);
+    p->pow_w = r.fr();
+    if (r.bad || nq > (len - r.off) / (32 * (p->w + q))) throw LspError(LSP_E_ARG, "malformed proof bytes");
+    p->queries.resize(nq);
+    for (auto& qq : p->queries) {
+        r.frs(qq.trow, p->w);
+        r.frs(qq.tpath, r.u32());
+        r.frs(qq.qrow, q);
+        r.frs(qq.qpath, r.u32());
+        qq.sib.resize(nr);
+        qq.fpath.resize(nr);
+        for (uint32_t k = 0; k < nr && !r.bad; ++k) {
+            qq.sib[k] = r.fr();
+            r.frs(qq.fpath[k], r.u32());
         }
-        if (!r.bad && r.off == len) return p.release();
+        if (r.bad) break;
     }
-    throw LspError(LSP_E_ARG, "malformed proof bytes");
+    if (r.bad || r.off != len) throw LspError(LSP_E_ARG, "malformed proof bytes");
+    return p.release();
 }
 
 namespace {
@@ -238,7 +236,7 @@ void proof_view(const lsp_proof& p, lsp_proof_view* v) {
 }
 
 lsp_proof* proof_from_view(const lsp_proof_view& v) {
-    // final_poly_len: a power of two (1 << log_final_poly_len) <= 2^20, the only
+    // final_poly_len: a power of two (1 << log_final_poly_len) <= 2^20, the
     // lengths the wire format's reader accepts, so every view that builds a
     // handle serializes to bytes lsp_proof_deserialize reads back
     if (v.width == 0 || v.width > (1u << 20) || v.log_quotient_chunks > 20 || v.degree_bits > 40 ||

@@ -57,15 +57,15 @@ bool mk_verify(const P2Host& p2, const Fr& root, size_t index, const Fr* leaf, s
 
 int verify_host(const lsp_ctx* ctx, const Air& air, const Fr* pub, size_t npub, const uint8_t* b, size_t n) {
     if (npub < 2) return 1;
-    if (n < 8 || std::memcmp(b, "LSPPRF01", 8) != 0) return 2;
+    if (n < 8 || std::memcmp(b, "LSPPRF02", 8) != 0) return 2;
     Reader r{b, n};
     r.off = 8;
-    const uint32_t log_h = r.u32(), log_q = r.u32(), w = r.u32(), nq = r.u32(), nr = r.u32();
+    const uint32_t log_h = r.u32(), log_q = r.u32(), w = r.u32(), nq = r.u32(), nr = r.u32(), nf = r.u32();
     if (r.bad || log_q != air.log_quotient_degree(ctx->public_degree) || nq != ctx->num_queries || log_h > 40 ||
         log_h < 1 || w <= air.max_col || w > (1u << 20))
         return 3;
     const uint32_t lb = ctx->log_blowup, logN = log_h + lb;
-    if (nr != logN - lb - ctx->log_final_poly_len) return 4;
+    if (nr != logN - lb - ctx->log_final_poly_len || nf != (1u << ctx->log_final_poly_len)) return 4;
     const size_t q = (size_t)1 << log_q, h = (size_t)1 << log_h;
     const size_t flen = (size_t)1 << ctx->log_final_poly_len;
     const Fr troot = r.fr(), qroot = r.fr();

@@ -1141,12 +1141,13 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
 
     /* ---- serialize */
     buf_t b = {NULL, 0, 0};
-    bput(&b, "LSPPRF01", 8);
+    bput(&b, "LSPPRF02", 8);
     bput_u32(&b, log_h);
     bput_u32(&b, log_q);
     bput_u32(&b, (uint32_t)w);
     bput_u32(&b, fri->num_queries);
     bput_u32(&b, nrounds);
+    bput_u32(&b, (uint32_t)flen);
     bput_fr(&b, &troot);
     bput_fr(&b, &qroot);
     for (size_t c = 0; c < w; ++c) bput_fr(&b, &ys_z[c]);
@@ -1231,9 +1232,11 @@ int lo_verify(const lo_params *p, const lo_fri *fri, const int32_t *air, size_t 
     int ncfg, K;
     if (parse_air(air, air_len, cfgs, &ncfg)) return -1;
     rd_t r = {proof, proof_len, 0, 0};
-    if (proof_len < 8 || memcmp(proof, "LSPPRF01", 8)) return 1;
+    if (proof_len < 8 || memcmp(proof, "LSPPRF02", 8)) return 1;
     r.off = 8;
-    uint32_t log_h = rd_u32(&r), log_q = rd_u32(&r), w = rd_u32(&r), nq = rd_u32(&r), nr = rd_u32(&r);
+    uint32_t log_h = rd_u32(&r), log_q = rd_u32(&r), w = rd_u32(&r), nq = rd_u32(&r), nr = rd_u32(&r),
+             nf = rd_u32(&r);
+    if (nf != 1) return 3; /* this verifier reads a 1-coefficient final polynomial only */
     int maxd = constraint_stats(cfgs, ncfg, public_degree, &K);
     if (maxd < 2) maxd = 2;
     uint32_t elq = 0;

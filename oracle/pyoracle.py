@@ -962,8 +962,8 @@ def verify(cfgs, proof: Proof, pub: List[int], pp: Poseidon2Params, fri: FriPara
 # ---------------------------------------------------------------------------
 def serialize_proof(p: Proof) -> bytes:
     fe = to_canon_bytes
-    out = bytearray(b"LSPPRF01")
-    out += struct.pack("<5I", p.degree_bits, p.log_q, p.width, len(p.queries), len(p.fri_roots))
+    out = bytearray(b"LSPPRF02")
+    out += struct.pack("<6I", p.degree_bits, p.log_q, p.width, len(p.queries), len(p.fri_roots), 1)
     out += fe(p.trace_root) + fe(p.quotient_root)
     for v in p.trace_local + p.trace_next + p.quotient_chunks + p.fri_roots:
         out += fe(v)
@@ -988,10 +988,11 @@ def serialize_proof(p: Proof) -> bytes:
 
 
 def deserialize_proof(b: bytes) -> Proof:
-    assert b[:8] == b"LSPPRF01"
+    assert b[:8] == b"LSPPRF02"
     off = 8
-    degree_bits, log_q, w, nq, nr = struct.unpack_from("<5I", b, off)
-    off += 20
+    degree_bits, log_q, w, nq, nr, nf = struct.unpack_from("<6I", b, off)
+    assert nf == 1, "this oracle handles a 1-coefficient final polynomial"
+    off += 24
 
     def fe():
         nonlocal off

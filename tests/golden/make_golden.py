@@ -28,6 +28,13 @@ def main():
     g["poseidon2_012"] = [hex(x) for x in O.permute([0, 1, 2], s.perm)]
     g["hash_iter_range"] = {str(w): hex(O.hash_iter(list(range(w)), s.perm)) for w in range(0, 6)}
     g["compress_1_2"] = hex(O.compress(1, 2, s.perm))
+    # U2/U3 as parameters (lsp_params.internal_diag / external_mds): one
+    # non-default internal diagonal and external matrix
+    diag, mds = (3, 5, O.P - 7), (5, 7, 1, 3, 2, 9, 4, 4, O.P - 1)
+    s.perm.int_diag, s.perm.ext_mds = diag, mds
+    g["poseidon2_012_layers"] = {"int_diag": [hex(x) for x in diag], "ext_mds": [hex(x) for x in mds],
+                                 "out": [hex(x) for x in O.permute([0, 1, 2], s.perm)]}
+    s.perm.int_diag = s.perm.ext_mds = None
     col = [pow(3, i, O.P) for i in range(4)]
     g["lde_col_3pow_h4_b3"] = [hex(x) for x in O.coset_lde_column(col, 3, O.GENERATOR)]
     g["proofs"] = {}

@@ -53,7 +53,7 @@ def test_config_matches_oracle(oracle_lib, kw, log_n, ncols):
             bad = bytearray(got)
             nr = log_n - fri.get("log_final_poly_len", 0)      # FRI rounds
             q = 1 << log_q
-            off = 8 + 20 + 64 + 32 * (2 * (2 * ncols + 2) + q) + 32 * nr + 32  # second final coefficient
+            off = 8 + 24 + 64 + 32 * (2 * (2 * ncols + 2) + q) + 32 * nr + 32  # second final coefficient
             bad[off] ^= 1
             assert not ctx.verify(bytes(bad), permutation_air(ncols), pub)
 

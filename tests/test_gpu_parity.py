@@ -344,7 +344,7 @@ def test_prove_rejects_tampering(gpu_ctx, oracle_lib):
     s, p, trace, w = _perm_setup(6, 3, oracle_lib)
     air = permutation_air(3)
     pf = bytearray(gpu_ctx.prove(trace, air, _pub(p)))
-    for off in (8 + 20 + 5, 8 + 20 + 64 + 7, len(pf) // 2, len(pf) - 3):
+    for off in (8 + 24 + 5, 8 + 24 + 64 + 7, len(pf) // 2, len(pf) - 3):
         bad = bytearray(pf)
         bad[off] ^= 1
         assert not gpu_ctx.verify(bytes(bad), air, _pub(p))

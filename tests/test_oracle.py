@@ -104,6 +104,11 @@ def test_golden_setup_and_primitives():
     for w, hv in GOLDEN["hash_iter_range"].items():
         assert hex(O.hash_iter(list(range(int(w))), s.perm)) == hv
     assert hex(O.compress(1, 2, s.perm)) == GOLDEN["compress_1_2"]
+    lay = GOLDEN["poseidon2_012_layers"]
+    s.perm.int_diag = [int(x, 16) for x in lay["int_diag"]]
+    s.perm.ext_mds = [int(x, 16) for x in lay["ext_mds"]]
+    assert [hex(x) for x in O.permute([0, 1, 2], s.perm)] == lay["out"]
+    s.perm.int_diag = s.perm.ext_mds = None
     col = [pow(3, i, O.P) for i in range(4)]
     assert [hex(x) for x in O.coset_lde_column(col, 3, O.GENERATOR)] == GOLDEN["lde_col_3pow_h4_b3"]
 

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -104,11 +105,30 @@ struct RcclComm : Comm {
     ~RcclComm() override {
         if (comm) rccl().destroy(comm);
     }
+    // Payloads are whole field elements (32-byte multiples): 64-bit words keep
+    // the element counts small (a 2^26-row proof's coefficient blocks are 2 GiB
+    // per rank), and broadcasts go in <= 1 GiB pieces
+    static ncclDataType_t dtype(size_t bytes, size_t& count) {
+        if (bytes % 8 == 0) {
+            count = bytes / 8;
+            return ncclUint64;
+        }
+        count = bytes;
+        return ncclUint8;
+    }
     void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
-        LSP_RCCL(rccl().all_gather(send, recv, bytes, ncclUint8, comm, ctx->stream));
+        size_t n;
+        const ncclDataType_t t = dtype(bytes, n);
+        LSP_RCCL(rccl().all_gather(send, recv, n, t, comm, ctx->stream));
     }
     void bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) override {
-        LSP_RCCL(rccl().broadcast(buf, buf, bytes, ncclUint8, root, comm, ctx->stream));
+        constexpr size_t piece = (size_t)1 << 30;
+        for (size_t off = 0; off < bytes; off += piece) {
+            size_t n;
+            const ncclDataType_t t = dtype(std::min(piece, bytes - off), n);
+            char* p = (char*)buf + off;
+            LSP_RCCL(rccl().broadcast(p, p, n, t, root, comm, ctx->stream));
+        }
     }
 };
 }  // namespace

@@ -175,3 +175,24 @@ def test_gpu_proof_generic_layers_matches_oracle(product_lib, oracle_lib, case, 
         proof = ctx.prove(trace, permutation_air(3), _pub(s))
         assert proof == expect
         assert ctx.verify(proof, permutation_air(3), _pub(s))
+
+
+@pytest.mark.gpu
+def test_gpu_sharded_proof_generic_layers(product_lib, oracle_lib):
+    """the sharded prover (4 virtual ranks: subtree roots, the split inverse
+    NTTs' exchanges, host tree tops per rank) with non-default constants and
+    layers equals the oracle's proof"""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import ProverGroup
+    s = _setup("both")
+    p = _cref_params(oracle_lib, s)
+    logn = 12
+    tb, w = oracle_lib.gen_perm_trace(p, logn, 3)
+    expect = oracle_lib.prove(p, tb, 1 << logn, w, oracle_lib.perm_air(3))
+    trace = np.frombuffer(tb.raw, dtype=np.uint64).reshape(1 << logn, w, 4).copy()
+    ctxs = [_ctx(s, 0) for _ in range(4)]
+    try:
+        assert ProverGroup(ctxs).prove(trace, permutation_air(3), _pub(s)) == expect
+    finally:
+        for c in ctxs:
+            c.close()

@@ -85,7 +85,7 @@ def test_full_size_lde_tree_and_proof(gpu_ctx, oracle_lib, log_n):
 
     # ---- the trace tree (fine-grained path) against the oracle and the proof
     root, tree = MerkleTreeMmcs(gpu_ctx).commit([lde])
-    assert from_mont(root)[0] == int.from_bytes(proof[28:60], "little")
+    assert from_mont(root)[0] == int.from_bytes(proof[32:64], "little")  # after "LSPPRF02" and 6 u32 fields
     if log_n <= 19:  # the oracle's whole tree (21 M permutations on 16 threads)
         lay = np.zeros((2 * N - 1, 4), np.uint64)
         L.lo_merkle_commit(ctypes.byref(p), _p(lde), ctypes.c_size_t(N), ctypes.c_size_t(w), _p(lay), 16)

@@ -73,8 +73,10 @@ FRMUL_PEAK_GPS = SIMDS * 64 / 4 * NOMINAL_GHZ / MAD_PER_FR_MUL  # 307.2 G Fr-mul
 
 
 def _lib_src() -> str:
-    from linea_stark_prover_amd.build import source_hash
-    return source_hash()
+    """the stamp of the library being benched (build.library_hash); the
+    working tree's hash only for an unstamped library"""
+    from linea_stark_prover_amd.build import library_hash, source_hash
+    return library_hash() or source_hash()
 
 
 LIB_SRC = _lib_src()  # the build the committed PMC profiles must match

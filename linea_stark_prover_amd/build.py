@@ -21,6 +21,7 @@ CSRC = os.path.join(PKG, "csrc")
 BUILD = os.path.join(PKG, "_build")
 LIBDIR = os.path.join(PKG, "_lib")
 LIB = os.path.join(LIBDIR, "liblsp_hip.so")
+STAMP = LIB + ".src"  # source_hash() of the sources the library was linked from
 ARCH = os.environ.get("LSP_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
@@ -49,6 +50,18 @@ def source_hash() -> str:
         hsh.update(fh.read())
     hsh.update(" ".join(CFLAGS[:-1] + [ARCH]).encode())
     return hsh.hexdigest()[:16]
+
+
+def library_hash() -> str | None:
+    """source_hash() of the sources liblsp_hip.so was linked from (written next
+    to the library at link time), or None when the library has no stamp.  The
+    stamp travels with the library, so a profile taken on a GPU box names the
+    build that ran there even when the working tree has moved on."""
+    try:
+        with open(STAMP) as fh:
+            return fh.read().strip() or None
+    except OSError:
+        return None
 
 
 def _headers():
@@ -98,6 +111,9 @@ def build(force: bool = False, jobs: int = None, verbose: bool = True) -> str:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         if verbose:
             print(f"[lsp build] linked {LIB}", flush=True)
+    if library_hash() != source_hash():
+        with open(STAMP, "w") as fh:
+            fh.write(source_hash() + "\n")
     return LIB
 
 

@@ -26,6 +26,7 @@
 // ark words reduced to < 2r; only the last forward pass writes canonical words.
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "fr29.hpp"
 #include "k_common.hpp"
@@ -154,7 +155,7 @@ struct TileLds {
 //
 // DIF stages s (distance D) and s + 1 (D/2) on v0..v3 = positions t0, t0 + D/2,
 // t0 + D, t0 + 3D/2: wA = w(s, t0), wA2 = w(s, t0 + D/2), wB = w(s + 1, t0)
-// (= w(s + 1, t0 + D)); trivB: stage s + 1 is the transform's last (w = 1).
+// (= w(s + 1, t0 + D)); TRIV: stage s + 1 is the transform's last (w = 1).
 // u0 stays carry-free (limbs < 2^30): as the minuend of f29_sub32 it makes
 // limbs < 2^31 and column sums < 2^63.74 in the product by wB
 // (tools/gen_fr29mul.py --bound), and f29_reduce takes it as it is (its
@@ -168,40 +169,63 @@ __device__ __forceinline__ F29 red(const F29& v, const uint4* __restrict__ qt) {
     return qt ? f29_reduce_qt(v, qt) : f29_reduce(v);
 }
 
+template <bool TRIV>
 __device__ __forceinline__ void dif4(F29& v0, F29& v1, F29& v2, F29& v3, const F29& wA, const F29& wA2,
-                                     const F29& wB, bool trivB, const uint4* __restrict__ qt) {
+                                     const F29& wB, const uint4* __restrict__ qt) {
     const F29 u0 = f29_lazy2(v0, v2);                  // < 16.6 r, limbs < 2^30
-    const F29 u2 = f29_mul(f29_sub16(v0, v2), wA);    // < 8.06 r
     const F29 u1 = f29_norm(f29_lazy2(v1, v3));
     const F29 u3 = f29_mul(f29_sub16(v1, v3), wA2);
-    v0 = red(f29_lazy2(u0, u1), qt);                  // < 2 r
-    v2 = red(f29_lazy2(u2, u3), qt);
-    if (trivB) {
+    if constexpr (TRIV) {
+        // the transform's last two stages: the group starts at an even row, so
+        // wA = w_4^0 = 1 as well and u2 needs no product.  u2 = sub16(v0, v2):
+        // limbs < 1.5 2^30, < 24.3 r; sub16(u2, u3) is dit4's sub16 of a sub16
+        // (limbs < 2.42 2^30, < 40.3 r), which both reductions take
+        const F29 u2 = f29_sub16(v0, v2);
+        v0 = red(f29_lazy2(u0, u1), qt);
+        v2 = red(f29_lazy2(u2, u3), qt);
         v1 = red(f29_sub32(u0, u1), qt);
         v3 = red(f29_sub16(u2, u3), qt);
     } else {
-        v1 = f29_mul(f29_sub32(u0, u1), wB);          // < 48.6 r in -> < 8.11 r
+        const F29 u2 = f29_mul(f29_sub16(v0, v2), wA);  // < 8.06 r
+        v0 = red(f29_lazy2(u0, u1), qt);                // < 2 r
+        v2 = red(f29_lazy2(u2, u3), qt);
+        v1 = f29_mul(f29_sub32(u0, u1), wB);            // < 48.6 r in -> < 8.11 r
         v3 = f29_mul(f29_sub16(u2, u3), wB);
     }
 }
 
 // DIT stages s (distance d) and s + 1 (2d) on v0..v3 = positions t0, t0 + d,
 // t0 + 2d, t0 + 3d: wA = w(s, t0) (= w(s, t0 + 2d)), wB = w(s + 1, t0),
-// wB2 = w(s + 1, t0 + d); trivA: stage s is the transform's first (w = 1).
+// wB2 = w(s + 1, t0 + d); TRIV: stage s is the transform's first (w = 1).
+template <bool TRIV>
 __device__ __forceinline__ void dit4(F29& v0, F29& v1, F29& v2, F29& v3, const F29& wA, const F29& wB,
-                                     const F29& wB2, bool trivA, const uint4* __restrict__ qt) {
-    const F29 p1 = trivA ? v1 : f29_mul(v1, wA);      // < 8.3 r
-    const F29 p3 = trivA ? v3 : f29_mul(v3, wA);
-    const F29 u0 = f29_lazy2(v0, p1);                 // limbs < 2^30, < 16.6 r
-    const F29 u1 = f29_sub16(v0, p1);                 // limbs < 1.5 2^30, < 24.6 r
-    const F29 u2 = f29_lazy2(v2, p3);
-    const F29 u3 = f29_sub16(v2, p3);
-    const F29 q2 = f29_mul(u2, wB);                   // < 8.07 r
-    const F29 q3 = f29_mul(u3, wB2);
-    v0 = red(f29_lazy2(u0, q2), qt);                  // < 2 r
-    v2 = red(f29_sub16(u0, q2), qt);
-    v1 = red(f29_lazy2(u1, q3), qt);
-    v3 = red(f29_sub16(u1, q3), qt);                  // limbs < 2.42 2^30
+                                     const F29& wB2, const uint4* __restrict__ qt) {
+    if constexpr (TRIV) {
+        // the transform's first two stages: the group starts at a row = 0 mod 4,
+        // so wB = w_4^0 = 1 as well.  u2 = v2 + v3 is normalised (< 16.6 r) to be
+        // the subtrahend of f29_sub32 (u0 + 32 r - u2: limbs < 2^31, < 48.6 r)
+        const F29 u0 = f29_lazy2(v0, v1);
+        const F29 u1 = f29_sub16(v0, v1);
+        const F29 u2 = f29_norm(f29_lazy2(v2, v3));
+        const F29 q3 = f29_mul(f29_sub16(v2, v3), wB2);
+        v0 = red(f29_lazy2(u0, u2), qt);
+        v2 = red(f29_sub32(u0, u2), qt);
+        v1 = red(f29_lazy2(u1, q3), qt);
+        v3 = red(f29_sub16(u1, q3), qt);
+    } else {
+        const F29 p1 = f29_mul(v1, wA);                 // < 8.3 r
+        const F29 p3 = f29_mul(v3, wA);
+        const F29 u0 = f29_lazy2(v0, p1);               // limbs < 2^30, < 16.6 r
+        const F29 u1 = f29_sub16(v0, p1);               // limbs < 1.5 2^30, < 24.6 r
+        const F29 u2 = f29_lazy2(v2, p3);
+        const F29 u3 = f29_sub16(v2, p3);
+        const F29 q2 = f29_mul(u2, wB);                 // < 8.07 r
+        const F29 q3 = f29_mul(u3, wB2);
+        v0 = red(f29_lazy2(u0, q2), qt);                // < 2 r
+        v2 = red(f29_sub16(u0, q2), qt);
+        v1 = red(f29_lazy2(u1, q3), qt);
+        v3 = red(f29_sub16(u1, q3), qt);                // limbs < 2.42 2^30
+    }
 }
 
 // One tile: 2^k positions x 2^logG groups x 2^LOGCW columns (power-of-two
@@ -279,24 +303,40 @@ __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOG
         // the quad's members are t0 + m 2^b: DIF distances 2^(b+1), 2^b; DIT 2^b, 2^(b+1)
         const uint32_t b = DIF ? (k - 2 - j) : j;
         const uint32_t bmask = (1u << b) - 1;
-        const bool triv = DIF ? (s + 1 == logH - 1) : (s == 0);
-        for (uint32_t qd = threadIdx.x; qd < (n_el >> 2); qd += NTT_THREADS) {
-            const uint32_t c = qd & (CW - 1);
-            const uint32_t pg = qd >> LOGCW;
-            const uint32_t g = pg & (G - 1), pp = pg >> gm.logG;
-            const uint32_t t0 = ((pp & ~bmask) << 2) | (pp & bmask);
-            const uint32_t e0 = (t0 << cshift) + (g << LOGCW) + c, de = (1u << b) << cshift;
-            F29 v0 = T.get(e0), v1 = T.get(e0 + de), v2 = T.get(e0 + 2 * de), v3 = T.get(e0 + 3 * de);
-            const uint32_t r0 = gm.row_of(t0, g), dr = (1u << b) << gm.logL;
-            if (DIF)
-                dif4(v0, v1, v2, v3, tw_at(r0, s), tw_at(r0 + dr, s), triv ? v0 : tw_at(r0, s + 1), triv, qt);
-            else
-                dit4(v0, v1, v2, v3, triv ? v0 : tw_at(r0, s), tw_at(r0, s + 1), tw_at(r0 + dr, s + 1), triv, qt);
-            T.put(e0, v0);
-            T.put(e0 + de, v1);
-            T.put(e0 + 2 * de, v2);
-            T.put(e0 + 3 * de, v3);
-        }
+        // the group at the transform's trivial end (the DIT's first two stages,
+        // the DIF's last two) runs its own loop: one product instead of four
+        // (dif4 / dit4 with TRIV), and its own register allocation
+        auto groups = [&](auto triv_tag) {
+            constexpr bool TRIV = decltype(triv_tag)::value;
+            for (uint32_t qd = threadIdx.x; qd < (n_el >> 2); qd += NTT_THREADS) {
+                const uint32_t c = qd & (CW - 1);
+                const uint32_t pg = qd >> LOGCW;
+                const uint32_t g = pg & (G - 1), pp = pg >> gm.logG;
+                const uint32_t t0 = ((pp & ~bmask) << 2) | (pp & bmask);
+                const uint32_t e0 = (t0 << cshift) + (g << LOGCW) + c, de = (1u << b) << cshift;
+                F29 v0 = T.get(e0), v1 = T.get(e0 + de), v2 = T.get(e0 + 2 * de), v3 = T.get(e0 + 3 * de);
+                const uint32_t r0 = gm.row_of(t0, g), dr = (1u << b) << gm.logL;
+                if constexpr (DIF) {
+                    if constexpr (TRIV)
+                        dif4<true>(v0, v1, v2, v3, v0, tw_at(r0 + dr, s), v0, qt);
+                    else
+                        dif4<false>(v0, v1, v2, v3, tw_at(r0, s), tw_at(r0 + dr, s), tw_at(r0, s + 1), qt);
+                } else {
+                    if constexpr (TRIV)
+                        dit4<true>(v0, v1, v2, v3, v0, v0, tw_at(r0 + dr, s + 1), qt);
+                    else
+                        dit4<false>(v0, v1, v2, v3, tw_at(r0, s), tw_at(r0, s + 1), tw_at(r0 + dr, s + 1), qt);
+                }
+                T.put(e0, v0);
+                T.put(e0 + de, v1);
+                T.put(e0 + 2 * de, v2);
+                T.put(e0 + 3 * de, v3);
+            }
+        };
+        if (DIF ? (s + 1 == logH - 1) : (s == 0))
+            groups(std::true_type{});
+        else
+            groups(std::false_type{});
         __syncthreads();
     }
     if (j < k) {  // the last stage alone (odd k)

@@ -142,3 +142,35 @@ def test_sub16_of_sub16_limbs():
     a = [MASK + L16[i] for i in range(8)]
     b = [x + L16[i] for i, x in enumerate(a)]
     assert max(b) < int(2.42 * (1 << 30)) < 3 * (1 << 30) - 8
+
+
+@pytest.mark.parametrize("red", [f29_reduce, f29_reduce_qt])
+def test_trivial_end_groups(red):
+    """the radix-4 groups at the trivial end of a transform skip the w_4^0
+    product (k_ntt.hip dif4 / dit4 with triv): dif4 reduces sub16(v0, v2) +- u3
+    unreduced, dit4 reduces u0 + 32r - norm(v2 + v3); worst limbs, values at
+    the bounds the comments state"""
+    rng = random.Random(17)
+    for _ in range(300):
+        v0, v2 = rng.randrange(int(8.3 * R)), rng.randrange(int(8.3 * R))
+        u3 = rng.randrange(int(8.06 * R))
+        # dif4: u2 = v0 + 16r - v2 limb-wise, normalised operands
+        u2 = [a + L16[i] - b for i, (a, b) in enumerate(zip(limbs(v0), limbs(v2)))]
+        s = [a + b for a, b in zip(u2, limbs(u3))]
+        d = [a + L16[i] - b for i, (a, b) in enumerate(zip(u2, limbs(u3)))]
+        assert max(s[:8]) < 1 << 31 and max(d[:8]) < int(2.42 * (1 << 30))
+        assert val(s) < 64 * R and val(d) < 64 * R
+        check_reduced(red(s), v0 - v2 + u3)
+        check_reduced(red(d), v0 - v2 - u3)
+        # dit4: u0 = v0 + v1 carry-free (limbs < 2^30), u2 = v2 + v3 normalised
+        v1, v3 = rng.randrange(int(8.3 * R)), rng.randrange(int(8.3 * R))
+        u0 = [a + b for a, b in zip(limbs(v0), limbs(v1))]
+        u2v = v2 + v3
+        e = [a + L32[i] - b for i, (a, b) in enumerate(zip(u0, limbs(u2v)))]
+        assert min(e) >= 0 and max(e[:8]) < 1 << 31 and val(e) < 64 * R
+        check_reduced(red(e), v0 + v1 - u2v)
+    # extremes: every operand limb at its cap
+    a = [MASK + L16[i] + MASK for i in range(8)]
+    assert max(a) < 1 << 31
+    b = [(1 << 30) - 2 + L32[i] for i in range(8)]
+    assert max(b) < 1 << 31

@@ -6,7 +6,16 @@ Writes a JSON summary for the last (steady-state) LDE call."""
 import csv, json, os, sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from linea_stark_prover_amd.build import source_hash
+from linea_stark_prover_amd.build import library_hash, source_hash
+
+def run_stamp(run_dir):
+    """the library stamp the box recorded for this run (tools/pmc_stamp.sh
+    copies liblsp_hip.so.src there), else the local library's"""
+    f = os.path.join(run_dir, "lib_src_sha16.txt")
+    if os.path.exists(f):
+        return open(f).read().strip()
+    return library_hash() or source_hash()
+
 
 def per_dispatch(path):
     out = {}
@@ -51,5 +60,5 @@ res = {"kernel": "coset_lde_batch (row-major: inverse DIT pass(es), the fused in
                        "fetch_bytes_x2": fetch[k][1] * 2048, "write_bytes": write.get(k, [0, 0])[1] * 1024}
                       for k in kern],
        "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE separate passes on tools/lde_probe.py; FETCH x2 (gfx950)",
-       "lib_src_sha16": source_hash()}
+       "lib_src_sha16": run_stamp(os.path.dirname(os.path.dirname(os.path.abspath(sys.argv[1]))))}
 print(json.dumps(res, indent=1))

@@ -48,8 +48,9 @@ rows.sort(reverse=True)
 if len(sys.argv) > 2:  # JSON for bench.py (profiles/*_valu_pmc.json)
     import json
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from linea_stark_prover_amd.build import source_hash
-    json.dump({"lib_src_sha16": source_hash(),
+    from linea_stark_prover_amd.build import library_hash, source_hash
+    stamp = os.path.join(os.path.dirname(os.path.abspath(root)), "lib_src_sha16.txt")
+    json.dump({"lib_src_sha16": open(stamp).read().strip() if os.path.exists(stamp) else (library_hash() or source_hash()),
                "method": "rocprofv3 --pmc passes (tools/pmc_valu.sh) over tools/time_prove.py 19; "
                          "valu_issue = SQ_ACTIVE_INST_VALU x 4 (all waves) / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): "
                          "the share of SIMD cycles issuing VALU; valu_issue_x4 = SQ_INSTS_VALU x 4 / (same) "

@@ -196,20 +196,25 @@ __device__ __forceinline__ bool rec_enabled(uint32_t r, size_t n, const Fr* afil
 
 // the slot of comb[r]'s key (linear probing; insert claims an empty slot
 // with a CAS -- slots never change once claimed, so every thread with the
-// same key ends in the same slot).  Without insert the key must be present.
+// same key ends in the same slot).  Without insert the key is looked up: an
+// empty slot ends the probe (H_EMPTY, absent).  Every probe ends within the
+// table's mask + 1 slots: the table has at least twice as many slots as
+// records (occ_capacity), and a full sweep returns H_EMPTY rather than spin.
 __device__ __forceinline__ uint32_t occ_slot(const Fr* __restrict__ comb, uint32_t r, uint32_t* rep, uint32_t mask,
                                              bool insert) {
     const Fr key = comb[r];
     uint32_t h = key_hash(key) & mask;
-    for (;;) {
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
         uint32_t cur = __hip_atomic_load(rep + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == H_EMPTY && insert) {
+        if (cur == H_EMPTY) {
+            if (!insert) return H_EMPTY;
             cur = atomicCAS(rep + h, H_EMPTY, r);
             if (cur == H_EMPTY) return h;
         }
-        if (cur != H_EMPTY && (cur == r || fr_eq(comb[cur], key))) return h;
+        if (cur == r || fr_eq(comb[cur], key)) return h;
         h = (h + 1) & mask;
     }
+    return H_EMPTY;
 }
 
 // enabled A rows count their key; enabled B entries record their (row, table)
@@ -221,6 +226,7 @@ __global__ __launch_bounds__(256) void k_occ_insert(const Fr* __restrict__ comb,
     const size_t r = gtid();
     if (r >= m || !rec_enabled((uint32_t)r, n, afil, bfil)) return;
     const uint32_t h = occ_slot(comb, (uint32_t)r, rep, mask, true);
+    if (h == H_EMPTY) return;  // (a full table: excluded by occ_capacity)
     if (r < n) {
         atomicAdd(cnt + h, 1u);
     } else {
@@ -238,6 +244,7 @@ __global__ __launch_bounds__(256) void k_occ_assign(const Fr* __restrict__ comb,
     const size_t j = gtid();  // B entry t n + i
     if (j >= n * nt || !fr_nonzero(bfil[j])) return;
     const uint32_t h = occ_slot(comb, (uint32_t)(n + j), rep, mask, false);
+    if (h == H_EMPTY) return;  // (every enabled B entry was inserted by k_occ_insert)
     const size_t t = j / n, i = j - t * n;
     if (minb[h] == (unsigned long long)(i * nt + t)) occ[j] = cnt[h];
 }
@@ -369,7 +376,9 @@ hipError_t launch_fr_scan(const Fr* in, Fr* out, size_t n, bool product, void* s
 hipError_t launch_lookup_occurrences(const Fr* comb, size_t n, uint32_t nt, const Fr* afil, const Fr* bfil,
                                      uint32_t* occ, void* scratch, size_t scratch_bytes, hipStream_t st) {
     const size_t m = n * (1 + (size_t)nt);
-    if (m >= H_EMPTY) return hipErrorInvalidValue;  // record ids are 32-bit
+    // record ids are 32-bit and slot ids must stay below H_EMPTY: <= 2^30 records
+    // (a table of <= 2^31 slots)
+    if (m > (1ull << 30)) return hipErrorInvalidValue;
     const size_t cap = occ_capacity(m);
     char* p = (char*)scratch;
     auto* minb = (unsigned long long*)p;  // 8-byte entries first (alignment)

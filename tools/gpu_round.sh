@@ -16,3 +16,6 @@ cat gpurun_out/bench_$TAG.json
 echo "=== rocprof"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o bench -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --inflight 0 --shard-leg none --batch-leg none --shape-leg none --no-host-trace-leg > gpurun_out/prof_bench_$TAG.json 2> gpurun_out/prof_$TAG.err || { tail -20 gpurun_out/prof_$TAG.err; exit 1; }
 echo done
+echo "=== pmc (stamped with this library)"
+bash tools/pmc_stamp.sh pmc_$TAG || exit 1
+echo pmc done

@@ -219,12 +219,15 @@ int lsp_batch_inverse(lsp_ctx *ctx, const lsp_fr *in, size_t n, lsp_fr *out, int
 int lsp_prove(lsp_ctx *ctx, const lsp_fr *trace, size_t h, size_t w, const int32_t *air, size_t air_len,
               const lsp_fr *public_values, size_t npub, int mem, lsp_proof **out);
 /* Sharded prove: one proof over G = 2^b ranks,
- * G <= 2^log_blowup.  Rank g owns the LDE rows [g N/G, (g+1) N/G) -- whole
- * cosets of the bit-reversed LDE, so a whole subtree of each input Merkle
- * tree -- the quotient points whose rows it holds and a slice of every FRI
- * vector; ranks exchange subtree roots, the quotient chunks, the opened
- * values, short FRI vectors and the query openings.  The proof is
- * byte-identical to lsp_prove's.
+ * G <= 2^(log_blowup + 6) and at least 2 LDE rows per rank (LSP_E_ARG /
+ * LSP_E_SIZE otherwise).  Rank g owns the LDE rows [g N/G, (g+1) N/G) --
+ * whole cosets of the bit-reversed LDE while G <= 2^log_blowup, a sub-coset
+ * of N/G < h rows beyond, in either case a whole
+ * subtree of each input Merkle tree -- the quotient points whose rows it
+ * holds and a slice of every FRI vector; ranks exchange subtree roots, the
+ * trace coefficients, the quotient chunks, the opened values, short FRI
+ * vectors and the query openings.  The proof is byte-identical to
+ * lsp_prove's.
  * In-process group: rank g = ctxs[g]; distinct devices (one host process
  * driving the node's GPUs, exchanges device-to-device with peer access) or
  * the same device repeated (virtual ranks).  traces[g] is rank g's copy of

@@ -190,14 +190,11 @@ __global__ __launch_bounds__(256) void k_gather(const uint64_t* __restrict__ ptr
     if (i < n) out[i] = *reinterpret_cast<const Fr*>(ptrs[i]);
 }
 
-__global__ __launch_bounds__(256) void k_assemble_chunks(const Fr* __restrict__ stage, uint32_t logGq, size_t cpr,
-                                                         size_t h, Fr* __restrict__ out) {
-    const size_t t = gtid();
-    const size_t q = cpr << logGq;
-    if (t >= h * q) return;
-    const size_t k = t / q, j = t - k * q;
-    const size_t r = brev_bits(j & ((1ull << logGq) - 1), logGq), c = j >> logGq;
-    out[t] = stage[(r * h + k) * cpr + c];
+__global__ __launch_bounds__(256) void k_assemble_chunks(const Fr* __restrict__ stage, uint32_t logGq, size_t Sq,
+                                                         Fr* __restrict__ out) {
+    const size_t i = gtid();
+    if (i >= (Sq << logGq)) return;
+    out[i] = stage[brev_bits(i & ((1ull << logGq) - 1), logGq) * Sq + (i >> logGq)];
 }
 }  // namespace
 
@@ -248,9 +245,9 @@ hipError_t launch_gather(const uint64_t* ptrs, Fr* out, size_t n, hipStream_t st
     return hipGetLastError();
 }
 
-hipError_t launch_assemble_chunks(const Fr* stage, uint32_t logGq, size_t cpr, size_t h, Fr* out, hipStream_t st) {
-    const size_t n = h * (cpr << logGq);
-    hipLaunchKernelGGL(k_assemble_chunks, dim3(nblocks(n, 256)), dim3(256), 0, st, stage, logGq, cpr, h, out);
+hipError_t launch_assemble_chunks(const Fr* stage, uint32_t logGq, size_t Sq, Fr* out, hipStream_t st) {
+    const size_t n = Sq << logGq;
+    hipLaunchKernelGGL(k_assemble_chunks, dim3(nblocks(n, 256)), dim3(256), 0, st, stage, logGq, Sq, out);
     return hipGetLastError();
 }
 

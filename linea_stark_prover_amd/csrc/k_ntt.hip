@@ -514,6 +514,26 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
     }
 }
 
+// A sub-coset's folded coefficients (launch_fold_subcoset): out[i][c] =
+// sum_t coef[i + t S][c] fac[c f + t].  Inputs as the inverse leaves them
+// (< 8.3 r), factors canonical in the 29-bit form; each product < 8.06 r,
+// the running sum reduced below 2 r after every addition, stored < 2 r.
+__global__ __launch_bounds__(256) void k_fold_subcoset(const Fr* __restrict__ coef, ColMap map, uint64_t H, uint64_t S,
+                                                       uint32_t w, uint32_t f, const Fr* __restrict__ fac,
+                                                       Fr* __restrict__ out) {
+    const size_t e = gtid();
+    if (e >= S * w) return;
+    const size_t i = e / w;
+    const uint32_t c = (uint32_t)(e - i * w);
+    F29 acc = f29_zero();
+    for (uint32_t t = 0; t < f; ++t) {
+        size_t si;
+        if (!src_at(map, H, (uint32_t)(i + t * S), c, si)) continue;  // a padding column
+        acc = f29_reduce(f29_lazy2(acc, f29_mul(f29_repack_in(coef[si]), f29_repack_in(fac[(size_t)c * f + t]))));
+    }
+    out[e] = f29_store(acc, false);
+}
+
 // ark-form words -> the 29-bit Montgomery form x 2^261 mod r, canonical, packed
 // in 8 words (twiddle and twist tables of k_ntt_rm)
 __global__ __launch_bounds__(256) void k_to_f29form(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n) {
@@ -736,6 +756,14 @@ hipError_t launch_lde_coeffs(const Fr* coef, ColMap map, Fr* out, size_t w, uint
                              hipStream_t st) {
     return run_lde(LDE_FWD, coef, map, nullptr, out, w, logh, ncosets, nullptr, tw_fwd, twist, L1, L2, twist_per_col,
                    st);
+}
+
+hipError_t launch_fold_subcoset(const Fr* coef, ColMap map, size_t h, size_t S, uint32_t w, const Fr* fac, Fr* out,
+                                hipStream_t st) {
+    if (S == 0 || h % S != 0 || h / S > 64 || w == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_fold_subcoset, dim3(nblocks(S * w, 256)), dim3(256), 0, st, coef, map, (uint64_t)h,
+                       (uint64_t)S, w, (uint32_t)(h / S), fac, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_to_f29form(const Fr* in, Fr* out, size_t n, hipStream_t st) {

@@ -41,7 +41,7 @@ constexpr uint32_t RR_CHUNK = 3;  // 3 normalised products + a value < 2r: limbs
 __global__ __launch_bounds__(256) void k_interp_partial(const Fr* __restrict__ M, uint32_t w, size_t h,
                                                         const Fr* __restrict__ inv_den, Fr gen,
                                                         const Fr* __restrict__ tabN, uint32_t L1, uint32_t logN,
-                                                        Fr* __restrict__ partial) {
+                                                        Fr* __restrict__ partial, uint64_t row0) {
     __shared__ Fr red[256];
     __shared__ F29 sc[INTERP_ROWS];
     __shared__ uint4 qt[3 * F29_QTAB_N];
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void k_interp_partial(const Fr* __restrict__ M
     const size_t r0 = (size_t)blockIdx.x * INTERP_ROWS;
     const uint32_t nr = (uint32_t)min((size_t)INTERP_ROWS, h - r0);
     for (uint32_t e = threadIdx.x; e < nr; e += blockDim.x)
-        sc[e] = f29_from_fr(fr_mul(fr_mul(gen, pow2l(tabN, L1, brev_bits(r0 + e, logN))), inv_den[r0 + e]));
+        sc[e] = f29_from_fr(fr_mul(fr_mul(gen, pow2l(tabN, L1, brev_bits(row0 + r0 + e, logN))), inv_den[r0 + e]));
     __syncthreads();
     // the threads as R row lanes x W adjacent columns (W = min(w, 256)): one step
     // reads W adjacent elements of R consecutive rows, a contiguous run of the
@@ -232,10 +232,10 @@ hipError_t launch_shift_inverse(const Fr* inv_z, Fr* out, Fr c, uint32_t logN, u
 }
 
 hipError_t launch_interp_partial(const Fr* M, uint32_t w, size_t h, const Fr* inv_den, Fr gen, const Fr* tabN,
-                                 uint32_t L1, uint32_t logN, Fr* partial, uint32_t* nb, hipStream_t st) {
+                                 uint32_t L1, uint32_t logN, Fr* partial, uint32_t* nb, hipStream_t st, uint64_t row0) {
     *nb = (uint32_t)((h + INTERP_ROWS - 1) / INTERP_ROWS);
     hipLaunchKernelGGL(k_interp_partial, dim3(*nb), dim3(256), 0, st, M, w, h, inv_den, gen, tabN, L1, logN,
-                       partial);
+                       partial, row0);
     return hipGetLastError();
 }
 

@@ -78,7 +78,8 @@ __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
     const F29 last = F.mul(zh, F.mul(f29_from_fr(xm1), inv_den));  // Z_H / (x - w^-1)
     const F29 trans = xml29;                                         // x - w^-1
     const Fr* loc = a.lde + (brev_bits(i, a.logQ) - a.row0) * a.w;
-    const Fr* nxt = a.lde + (brev_bits((i + (1ull << a.log_q)) & (Q - 1), a.logQ) - a.row0) * a.w;
+    const Fr* nxt = a.lde_next ? a.lde_next + (brev_bits((i + (1ull << a.log_q)) & (Q - 1), a.logQ) - a.row0_next) * a.w
+                               : a.lde + (brev_bits((i + (1ull << a.log_q)) & (Q - 1), a.logQ) - a.row0) * a.w;
     const F29 ap = f29_from_fr(a.pub_alpha), dl = f29_from_fr(a.pub_delta), al = f29_from_fr(a.alpha);
     F29 acc = f29_zero();
 #define PUSH(X) acc = F.add(F.mul(acc, al), (X))

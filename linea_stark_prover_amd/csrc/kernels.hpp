@@ -57,6 +57,15 @@ hipError_t launch_intt(const Fr* in, ColMap map, Fr* X, size_t w, uint32_t logh,
 hipError_t launch_lde_coeffs(const Fr* coef, ColMap map, Fr* out, size_t w, uint32_t logh, uint32_t ncosets,
                              const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
                              hipStream_t st);
+// A sub-coset of the LDE (a sharded proof over more ranks than cosets):
+// out (S x w, row-major) = the h coefficients of every column folded to S,
+// out[i][c] = sum_t coef[i + t S][c] fac[c f + t] for t < f = h / S (coef read
+// through `map`, values as launch_intt leaves them; fac: the f factors
+// sigma_c^t / f of each column in the 29-bit form, launch_to_f29form).  The
+// size-S coset NTT of the folded column equals the degree < h polynomial on
+// that size-S coset when sigma_c = (its shift)^S.
+hipError_t launch_fold_subcoset(const Fr* coef, ColMap map, size_t h, size_t S, uint32_t w, const Fr* fac, Fr* out,
+                                hipStream_t st);
 // ark-form words -> the 29-bit Montgomery form (x 2^261 mod r), canonical, in place allowed
 hipError_t launch_to_f29form(const Fr* in, Fr* out, size_t n, hipStream_t st);
 // the same, unpacked into 9 x 29-bit limbs padded to 48 bytes (3 x uint4 per
@@ -128,7 +137,10 @@ hipError_t launch_gather(const uint64_t* ptrs, Fr* out, size_t n, hipStream_t st
 // Sharded quotient exchange: stage holds 2^logGq blocks of h x cpr values,
 // block r = chunks j = bitrev(r) + (c << logGq), c < cpr; out = the natural
 // h x q chunk matrix (q = cpr << logGq), out[k*q + j].
-hipError_t launch_assemble_chunks(const Fr* stage, uint32_t logGq, size_t cpr, size_t h, Fr* out, hipStream_t st);
+// out[i] = stage[bitrev(i mod Gq) Sq + i / Gq] for i < Q = Gq Sq: the h x q
+// quotient matrix (row k, chunk j = point k q + j) from the Gq ranks' slots of
+// Sq points each (rank r computed the points bitrev(r) + Gq m)
+hipError_t launch_assemble_chunks(const Fr* stage, uint32_t logGq, size_t Sq, Fr* out, hipStream_t st);
 
 // ----------------------------------------------------- k_witness.hip
 // (trace crate semantics; see k_witness.hip)
@@ -179,6 +191,10 @@ struct QuotientArgs {
     uint32_t log_step = 0;
     uint64_t row0 = 0;
     uint64_t n = 0;
+    // the next-row LDE rows (point i + q), from global row `row0_next` on;
+    // nullptr: in `lde` (every point's successor on the same rank)
+    const Fr* lde_next = nullptr;
+    uint64_t row0_next = 0;
 };
 // den[m] = (x_i - 1)(x_i - w_h^-1), x_i = GEN * w_Q^i, i = i0 + (m << log_step), m < n
 hipError_t launch_selector_denoms(const Fr* tabQ, uint32_t L1, Fr gen, Fr wh_inv, size_t n, Fr* den,
@@ -196,7 +212,8 @@ hipError_t launch_shift_inverse(const Fr* inv_z, Fr* out, Fr c, uint32_t logN, u
 // partial sums for barycentric interpolation over rows [0, h):
 // partial[b*w + c] = sum_{i in block b} M[i][c] * x_i * inv_den[i]
 hipError_t launch_interp_partial(const Fr* M, uint32_t w, size_t h, const Fr* inv_den, Fr gen, const Fr* tabN,
-                                 uint32_t L1, uint32_t logN, Fr* partial, uint32_t* nblocks, hipStream_t st);
+                                 uint32_t L1, uint32_t logN, Fr* partial, uint32_t* nblocks, hipStream_t st,
+                                 uint64_t row0 = 0);
 // out[c] = sum_b partial[b*w + c]
 hipError_t launch_sum_partials(const Fr* partial, uint32_t nblocks, uint32_t w, Fr* out, hipStream_t st);
 struct ReduceArgs {

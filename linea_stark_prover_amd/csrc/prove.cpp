@@ -192,6 +192,37 @@ static void lde_coeffs_device(lsp_ctx* ctx, const Fr* coef, ColMap map, size_t h
                               T.shared ? 0 : 1, ctx->stream));
 }
 
+// Block `blk` (S = N / 2^b rows, S < h) of the bit-reversed N-row LDE, when a
+// proof has more ranks than cosets: the evaluations on the sub-coset
+// c H_S, c = shift_c w_N^bitrev_b(blk).  The h coefficients of every column
+// fold to S (c'_i = sum_t c_(i + t S) c^(t S), SURVEY 8(e) step 6 without a
+// transpose), then one size-S coset NTT of the folded columns, which is
+// lde_coeffs_device with the LDE seen as 2^b blocks of S rows.  The fold also
+// divides by f = h / S, so the NTT's 1/S twist scale gives the 1/h the
+// coefficients (h * c_i, as the inverse leaves them) need.
+static void subcoset_lde(lsp_ctx* ctx, const Fr* coef, ColMap map, size_t h, size_t w, uint32_t logN, uint32_t b,
+                         uint32_t blk, const Fr* shifts_host, Fr* d_out, const std::string& tag) {
+    const size_t S = (size_t)1 << (logN - b), f = h / S;
+    LSP_REQUIRE(S < h && f <= 64 && S >= 2, LSP_E_ARG, "sub-coset outside 2 .. h/2 rows");
+    const Fr cb = fr_pow_u64(host_two_adic_generator(logN), host_bitrev(blk, b));
+    const Fr finv = host_inv_cached(fr_from_u64(f));
+    std::vector<Fr> fac(w * f);
+    for (size_t c = 0; c < w; ++c) {
+        const Fr sigma = fr_pow_u64(fr_mul(shifts_host[c], cb), S);
+        Fr x = finv;
+        for (size_t t = 0; t < f; ++t) {
+            fac[c * f + t] = x;
+            x = fr_mul(x, sigma);
+        }
+    }
+    Fr* dfac = ctx->fbuf(tag + "_fac", w * f);
+    ctx->h2d_async(tag + "_fac_h", dfac, fac.data(), fac.size() * sizeof(Fr));
+    LSP_HIP(launch_to_f29form(dfac, dfac, w * f, ctx->stream));
+    Fr* folded = ctx->fbuf(tag + "_fold", S * w);
+    LSP_HIP(launch_fold_subcoset(coef, map, h, S, (uint32_t)w, dfac, folded, ctx->stream));
+    lde_coeffs_device(ctx, folded, ColMap::plain((uint32_t)w), S, w, b, shifts_host, d_out, blk, 1);
+}
+
 // A sharded proof splits the inverse NTTs by columns (rank g inverts the
 // columns bitrev(g) + G k and the coefficients are exchanged) instead of every
 // rank inverting every column; LSP_SHARD_SPLIT_INTT=0 restores the redundant
@@ -562,10 +593,14 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
     LSP_REQUIRE(logN <= 40, LSP_E_SIZE, "trace too large");
     const uint32_t G = (uint32_t)comm.size, g = (uint32_t)comm.rank;
     const uint32_t b = log2_exact(G);
-    LSP_REQUIRE(b <= lb, LSP_E_ARG, "a proof shards over at most 2^log_blowup ranks");
+    LSP_REQUIRE(b <= lb + 6, LSP_E_ARG, "a proof shards over at most 2^(log_blowup + 6) ranks");
+    LSP_REQUIRE(b < logN, LSP_E_SIZE, "more ranks than LDE rows / 2");
     const uint32_t logS = logN - b;
     const size_t S = N >> b, row0 = (size_t)g * S;
-    const uint32_t nk = 1u << (lb - b), k0 = g * nk;  // this rank's cosets
+    // G <= 2^lb: rank g owns the whole cosets [k0, k0 + nk).  G > 2^lb (sub): a
+    // sub-coset of S < h rows, folded from the coefficients (subcoset_lde)
+    const bool sub = b > lb;
+    const uint32_t nk = sub ? 1u : 1u << (lb - b), k0 = sub ? g : g * nk;
     hipStream_t st = ctx->stream;
     const Fr GEN = host_generator();
     const Fr one = fr_one();
@@ -595,6 +630,8 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         T.begin("coset_lde_batch");
         span("coset_lde_batch", w, h, (int)lb);
         const bool split = G > 1 && split_intt();
+        const Fr* tcoef = nullptr;  // h * coefficients of the trace (split or sub), read through tmap
+        ColMap tmap;
         if (split) {
             // rank g inverts the columns bitrev(g) + G k (k < cg; columns past w
             // are zero padding), the ranks allgather the h x cg coefficient
@@ -607,10 +644,20 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             m.cstep = G;
             LSP_HIP(launch_intt(d_trace, m, xl, cg, log_h, ctx->twiddle29(log_h, true), st));
             comm.allgather(ctx, xl, coef, h * cg * sizeof(Fr));
-            lde_coeffs_device(ctx, coef, ColMap::blocked(b, cg), h, w, lb, shifts.data(), lde, k0, nk);
-        } else {
-            lde_device(ctx, d_trace, h, w, lb, shifts.data(), lde, k0, nk);
+            tcoef = coef;
+            tmap = ColMap::blocked(b, cg);
+        } else if (sub) {  // every rank inverts every column (LSP_SHARD_SPLIT_INTT=0)
+            Fr* coef = ctx->fbuf("t_coef", h * w);
+            LSP_HIP(launch_intt(d_trace, ColMap::plain((uint32_t)w), coef, w, log_h, ctx->twiddle29(log_h, true), st));
+            tcoef = coef;
+            tmap = ColMap::plain((uint32_t)w);
         }
+        if (sub)
+            subcoset_lde(ctx, tcoef, tmap, h, w, logN, b, g, shifts.data(), lde, "t_sub");
+        else if (split)
+            lde_coeffs_device(ctx, tcoef, tmap, h, w, lb, shifts.data(), lde, k0, nk);
+        else
+            lde_device(ctx, d_trace, h, w, lb, shifts.data(), lde, k0, nk);
         T.end("coset_lde_batch");
         Fr* tlay = ctx->fbuf("t_tree", 2 * S - 1);
         std::vector<std::vector<Fr>> ttop, qtop;
@@ -638,9 +685,26 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         // G = 1: the h x q chunk matrix.  G > 1: ranks g < Gq evaluate points
         // into their slot of the exchange buffer (split: into a local buffer,
         // whose inverse NTT goes to the slot)
-        Fr* qv = G == 1 || !split ? ctx->fbuf("q_values", Q) : nullptr;
+        // sub: a chunk spreads over Gq / q ranks, so the holders broadcast values
+        // and every rank inverts the assembled h x q matrix
+        const bool qsplit = split && !sub;
+        Fr* qv = G == 1 || !qsplit ? ctx->fbuf("q_values", Q) : nullptr;
         Fr* stage = G == 1 ? nullptr : ctx->fbuf("q_stage", Sq * Gq);
-        Fr* qloc = G == 1 ? qv : (g < Gq ? (split ? ctx->fbuf("q_vals_local", Sq) : stage + (size_t)g * Sq) : nullptr);
+        Fr* qloc = G == 1 ? qv : (g < Gq ? (qsplit ? ctx->fbuf("q_vals_local", Sq) : stage + (size_t)g * Sq) : nullptr);
+        // point i + q (the next trace row) of this rank's points i = i0 + Gq m:
+        // on this rank when Gq <= q; else all on the rank with residue
+        // (i0 + q) mod Gq, whose LDE rows this rank computes itself
+        const Fr* lde_next = nullptr;
+        uint64_t row0_next = 0;
+        if (sub && row0 < Q) {
+            const uint32_t gn = (uint32_t)host_bitrev((host_bitrev(g, logGq) + q) & (Gq - 1), logGq);
+            if (gn != g) {
+                Fr* nl = ctx->fbuf("t_lde_next", S * w);
+                subcoset_lde(ctx, tcoef, tmap, h, w, logN, b, gn, shifts.data(), nl, "t_next");
+                lde_next = nl;
+                row0_next = (uint64_t)gn * S;
+            }
+        }
         std::vector<Fr> zh(q), izh(q);
         if (row0 < Q) {
             const uint64_t i0 = host_bitrev(g, logGq);
@@ -694,6 +758,8 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             qa.log_step = logGq;
             qa.row0 = row0;
             qa.n = Sq;
+            qa.lde_next = lde_next;
+            qa.row0_next = row0_next;
             LSP_HIP(launch_quotient(qa, st));
         }
         if (G > 1) {
@@ -701,11 +767,11 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             // broadcast per holder (only the Gq holders send: Gq/G of an allgather's bytes).
             // split: the holder sends its chunks' coefficients (its own inverse
             // NTT), and no rank inverts the whole h x q matrix
-            if (split && g < Gq)
+            if (qsplit && g < Gq)
                 LSP_HIP(launch_intt(qloc, ColMap::plain((uint32_t)cpr), stage + (size_t)g * Sq, cpr, log_h,
                                     ctx->twiddle29(log_h, true), st));
             for (uint32_t r = 0; r < Gq; ++r) comm.bcast(ctx, stage + (size_t)r * Sq, Sq * sizeof(Fr), (int)r);
-            if (!split) LSP_HIP(launch_assemble_chunks(stage, logGq, cpr, h, qv, st));
+            if (!qsplit) LSP_HIP(launch_assemble_chunks(stage, logGq, Sq, qv, st));
         }
         T.end("compute quotient polynomial");
 
@@ -722,10 +788,15 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         Fr* qlde = ctx->fbuf("q_lde", S * q);
         T.begin("coset_lde_batch (quotient)");
         for (size_t j = 0; j < q; ++j) span("coset_lde_batch", 1, h, (int)lb);  // one launch, q independent columns
-        if (split)  // the chunk coefficients straight from the exchange buffer (column j in slot bitrev(j mod Gq))
+        if (qsplit) {  // the chunk coefficients straight from the exchange buffer (column j in slot bitrev(j mod Gq))
             lde_coeffs_device(ctx, stage, ColMap::blocked(logGq, (uint32_t)cpr), h, q, lb, shifts.data(), qlde, k0, nk);
-        else
+        } else if (sub) {
+            Fr* qc = ctx->fbuf("q_coef", h * q);
+            LSP_HIP(launch_intt(qv, ColMap::plain((uint32_t)q), qc, q, log_h, ctx->twiddle29(log_h, true), st));
+            subcoset_lde(ctx, qc, ColMap::plain((uint32_t)q), h, q, logN, b, g, shifts.data(), qlde, "q_sub");
+        } else {
             lde_device(ctx, qv, h, q, lb, shifts.data(), qlde, k0, nk);
+        }
         T.end("coset_lde_batch (quotient)");
         Fr* qlay = ctx->fbuf("q_tree", 2 * S - 1);
         proof->qroot = shard_root(ctx, comm, commit_device(ctx, one_mat(qlde, (uint32_t)q), S, qlay), qtop);
@@ -752,26 +823,47 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         LSP_REQUIRE(!fr_is_zero(den_prod), LSP_E_STATE, "zeta lies in the LDE domain");
         const Fr den_prod_inv = fr_inv(den_prod);
         LSP_HIP(launch_batch_inverse(dtmp, inv_z, S, st, ctx->bi_scratch(S), &den_prod_inv));
-        LSP_HIP(launch_shift_inverse(inv_z, inv_zn, wh_inv, logN, 1ull << lb, row0, S, st));
+        if (sub) {
+            // x w_h^-1 leaves a sub-coset (w_h is not in H_S): the zeta_next
+            // denominators are inverted on their own
+            const Fr dpn = fr_sub(fr_pow_u64(zeta_next, S), cS);
+            LSP_REQUIRE(!fr_is_zero(dpn), LSP_E_STATE, "zeta * w_h lies in the LDE domain");
+            const Fr dpn_inv = fr_inv(dpn);
+            LSP_HIP(launch_open_denoms(zeta_next, GEN, tabN, L1N, logN, S, dtmp, st, row0));
+            LSP_HIP(launch_batch_inverse(dtmp, inv_zn, S, st, ctx->bi_scratch(S), &dpn_inv));
+        } else {
+            LSP_HIP(launch_shift_inverse(inv_z, inv_zn, wh_inv, logN, 1ull << lb, row0, S, st));
+        }
         T.end("compute_inverse_denominators");
         T.begin("compute opened values with Lagrange interpolation");
         // barycentric sums on the low coset (first h rows: rank 0), then the host-side factor
         const size_t maxw = std::max(w, q);
         Fr* sums = ctx->fbuf("o_sums", 2 * w + q);
-        if (g == 0) {
-            Fr* partial = ctx->fbuf("o_partial", ((h + 1023) / 1024) * maxw);
+        const size_t nlow = std::min(S, h);  // this rank's rows of the low coset (sub: ranks 0 .. h/S - 1)
+        if (row0 < h) {
+            Fr* partial = ctx->fbuf("o_partial", ((nlow + 1023) / 1024) * maxw);
             uint32_t nb = 0;
-            LSP_HIP(launch_interp_partial(lde, (uint32_t)w, h, inv_z, GEN, tabN, L1N, logN, partial, &nb, st));
+            LSP_HIP(launch_interp_partial(lde, (uint32_t)w, nlow, inv_z, GEN, tabN, L1N, logN, partial, &nb, st, row0));
             LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)w, sums, st));
-            LSP_HIP(launch_interp_partial(lde, (uint32_t)w, h, inv_zn, GEN, tabN, L1N, logN, partial, &nb, st));
+            LSP_HIP(launch_interp_partial(lde, (uint32_t)w, nlow, inv_zn, GEN, tabN, L1N, logN, partial, &nb, st, row0));
             LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)w, sums + w, st));
-            LSP_HIP(launch_interp_partial(qlde, (uint32_t)q, h, inv_z, GEN, tabN, L1N, logN, partial, &nb, st));
+            LSP_HIP(launch_interp_partial(qlde, (uint32_t)q, nlow, inv_z, GEN, tabN, L1N, logN, partial, &nb, st, row0));
             LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)q, sums + 2 * w, st));
+        } else if (sub) {
+            LSP_HIP(hipMemsetAsync(sums, 0, (2 * w + q) * sizeof(Fr), st));
         }
-        if (G > 1) comm.bcast(ctx, sums, (2 * w + q) * sizeof(Fr), 0);
+        if (G > 1 && !sub) comm.bcast(ctx, sums, (2 * w + q) * sizeof(Fr), 0);
         Fr* hs = (Fr*)ctx->hbuf("o_sums_h", (2 * w + q) * sizeof(Fr));  // pinned
         LSP_HIP(hipMemcpyAsync(hs, sums, (2 * w + q) * sizeof(Fr), hipMemcpyDeviceToHost, st));
         LSP_HIP(hipStreamSynchronize(st));
+        if (sub) {  // the low coset's partial sums from its h / S ranks
+            const std::vector<Fr> all = comm.allgather_fr(ctx, hs, 2 * w + q);
+            for (size_t k = 0; k < 2 * w + q; ++k) {
+                Fr acc = fr_zero();
+                for (uint32_t r = 0; r < G; ++r) acc = fr_add(acc, all[(size_t)r * (2 * w + q) + k]);
+                hs[k] = acc;
+            }
+        }
         const Fr gh = fr_pow_u64(GEN, h);
         const Fr dinv = host_inv_cached(fr_mul(gh, fr_from_u64(h)));
         auto factor = [&](const Fr& z) { return fr_mul(fr_sub(fr_pow_u64(z, h), gh), dinv); };

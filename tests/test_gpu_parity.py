@@ -350,6 +350,34 @@ def test_prove_rejects_tampering(gpu_ctx, oracle_lib):
         assert not gpu_ctx.verify(bytes(bad), air, _pub(p))
 
 
+def test_prove_rejects_bad_arguments(gpu_ctx, oracle_lib):
+    """lsp_prove on malformed input returns an error code (the reference's
+    prover panics on these) and leaves the context usable: non-power-of-two
+    and one-row traces, a trace narrower than the AIR's columns, fewer than
+    two public values; then a good proof on the same context"""
+    import ctypes
+    from linea_stark_prover_amd import _lib
+    from linea_stark_prover_amd.air import permutation_air
+    s, p, trace, w = _perm_setup(4, 3, oracle_lib)
+    air = permutation_air(3)
+    pub = _pub(p)
+
+    def code(tr, pv):
+        with pytest.raises(_lib.LspError) as e:
+            gpu_ctx.prove(tr, air, pv)
+        return e.value.code
+
+    assert code(np.ascontiguousarray(trace[:12]), pub) == _lib.LSP_E_SIZE   # 12 rows
+    assert code(np.ascontiguousarray(trace[:1]), pub) == _lib.LSP_E_SIZE    # 1 row
+    assert code(np.ascontiguousarray(trace[:, : w - 1]), pub) == _lib.LSP_E_ARG  # column w-1 missing
+    assert code(trace, pub[:1]) == _lib.LSP_E_ARG                          # [alpha] only
+    desc = (ctypes.c_int32 * len(air.descriptor()))(*air.descriptor())
+    assert _lib.lib().lsp_prove(gpu_ctx.h, trace.ctypes.data, 16, w, desc, len(desc), pub.ctypes.data, 2,
+                                _lib.LSP_MEM_HOST, None) == _lib.LSP_E_ARG  # no output handle
+    got = gpu_ctx.prove(trace, air, pub)
+    assert got == oracle_lib.prove(p, trace.ctypes.data, 16, w, oracle_lib.perm_air(3))
+
+
 def test_prove_large_self_consistency(gpu_ctx):
     """2^16 rows: no oracle at this size in the default run; the product's
     verifier must accept and the LDE must agree with the trace on the low

@@ -1,4 +1,4 @@
-"""Sharded prove (lsp_prove_group): G = 2, 4, 8 ranks as virtual
+"""Sharded prove (lsp_prove_group): G = 2 .. 32 ranks as virtual
 ranks on one GPU (one context and one host thread each, exchanges through
 device copies).  The proof must be byte-identical to the single-rank proof,
 which the parity tests pin to the oracle."""
@@ -76,14 +76,50 @@ def test_group_device_resident_traces(gpu_ctx):
     assert got == gpu_ctx.prove(tr, permutation_air(3), pub)
 
 
+@pytest.mark.parametrize("G", [16, 32])
+@pytest.mark.parametrize("log_n,ncols", [(5, 3), (9, 3), (10, 6)])
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_more_ranks_than_cosets(gpu_ctx, monkeypatch, G, log_n, ncols, split):
+    """G > blowup: each rank owns a sub-coset of N/G < h
+    rows, folded from the coefficients; the quotient's next rows come from
+    the partner sub-coset, the chunk values are broadcast and inverted on
+    every rank, the low coset's partial sums are added across its ranks.
+    Byte-identical to the single-GPU proof, with the split inverse and
+    without it (LSP_SHARD_SPLIT_INTT=0)"""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import gen_permutation_trace
+    monkeypatch.setenv("LSP_SHARD_SPLIT_INTT", split)
+    monkeypatch.setenv("LSP_FRI_SHARD_MIN", "2")
+    a, d, _ = gpu_ctx.config.seeded()
+    tr = gen_permutation_trace(log_n, ncols, a, d)
+    pub = np.concatenate([a, d])
+    air = permutation_air(ncols)
+    single = gpu_ctx.prove(tr, air, pub)
+    grp, _ = _group(gpu_ctx, G)
+    assert grp.prove(tr, air, pub) == single
+
+
+def test_more_ranks_than_cosets_wide_air(gpu_ctx, monkeypatch):
+    """lookup + permutation configs (q = 8) over 16 ranks: every rank holds
+    quotient points, half a chunk each"""
+    from linea_stark_prover_amd.prover import gen_wide_trace
+    monkeypatch.setenv("LSP_FRI_SHARD_MIN", "4")
+    a, d, _ = gpu_ctx.config.seeded()
+    tr, air = gen_wide_trace(7, a, d, 2, 3, 2, 3, 6)
+    pub = np.concatenate([a, d])
+    single = gpu_ctx.prove(tr, air, pub)
+    grp, _ = _group(gpu_ctx, 16)
+    assert grp.prove(tr, air, pub) == single
+
+
 def test_group_rejects_too_many_ranks(gpu_ctx):
-    """G > blowup (16 > 8) cannot own whole cosets: a clean error on every rank"""
+    """fewer than 2 LDE rows per rank (2^2 rows, N = 32, G = 32): a clean error on every rank"""
     from linea_stark_prover_amd.air import permutation_air
     from linea_stark_prover_amd.prover import gen_permutation_trace
     a, d, _ = gpu_ctx.config.seeded()
-    tr = gen_permutation_trace(5, 3, a, d)
-    grp, _ = _group(gpu_ctx, 16)
-    with pytest.raises(RuntimeError, match="at most 2\\^log_blowup"):
+    tr = gen_permutation_trace(2, 3, a, d)
+    grp, _ = _group(gpu_ctx, 32)
+    with pytest.raises(RuntimeError, match="more ranks than LDE rows"):
         grp.prove(tr, permutation_air(3), np.concatenate([a, d]))
 
 

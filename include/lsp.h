@@ -337,6 +337,12 @@ int lsp_verify(const lsp_ctx *ctx, const int32_t *air, size_t air_len, const lsp
 /* per-phase device times of the last lsp_prove (ms), span names as in the
  * reference's bench.log */
 int lsp_last_timings(const lsp_ctx *ctx, double *ms, const char **names, size_t cap, size_t *n);
+/* Which phases the following proofs time (two device events each, ~0.3 ms
+ * of host API time per 2^19 proof for all of them): on = 0 none, on != 0
+ * with n_only = 0 all (the default), else only the phases named in only[]
+ * (span names as lsp_last_timings reports them).  lsp_last_timings reports
+ * the phases timed.  Proof bytes are the same either way. */
+int lsp_ctx_set_phase_timing(lsp_ctx *ctx, int on, const char *const *only, size_t n_only);
 /* the last lsp_prove's data-shaped operations in order, worded as the
  * reference's tracing spans with dims (bench.log:19-64), e.g.
  * "coset_lde_batch dims: 14x524288 | added_bits: 3",

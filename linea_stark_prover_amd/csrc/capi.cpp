@@ -779,6 +779,20 @@ int lsp_ctx_attach_loopback(lsp_ctx* ctx, int rank, int size) {
     });
 }
 
+int lsp_ctx_set_phase_timing(lsp_ctx* ctx, int on, const char* const* only, size_t n_only) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && (n_only == 0 || only), LSP_E_ARG, "null argument");
+        std::vector<std::string> names;
+        for (size_t i = 0; i < n_only; ++i) {
+            LSP_REQUIRE(only[i], LSP_E_ARG, "null phase name");
+            names.emplace_back(only[i]);
+        }
+        std::lock_guard<std::mutex> g(ctx->mu);
+        ctx->phase_timing = on != 0;
+        ctx->phase_only = std::move(names);
+    });
+}
+
 int lsp_ctx_mem_stats(lsp_ctx* ctx, size_t* pool_bytes, size_t* device_used, size_t* device_total) {
     return guarded(ctx, [&] {
         LSP_REQUIRE(ctx && pool_bytes && device_used && device_total, LSP_E_ARG, "null argument");

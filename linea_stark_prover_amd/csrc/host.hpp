@@ -274,6 +274,11 @@ struct lsp_ctx {
     std::map<std::string, hipEvent_t> stage_ev;  // last copy out of each h2d_async staging buffer
     hipEvent_t ev_near = nullptr, ev_top = nullptr;  // tree-top hand-off (prove.cpp commit_device)
     std::vector<hipEvent_t> event_pool;               // phase-timer events, reused across proofs
+    // per-phase device timings of lsp_prove (lsp_last_timings): two events per
+    // phase, ~0.3 ms of host API time per 2^19 proof; lsp_ctx_set_phase_timing
+    // (off, or only the named phases)
+    bool phase_timing = true;
+    std::vector<std::string> phase_only;
     std::map<std::pair<uint32_t, int>, uint4*> twiddles;
     std::map<std::string, const lsp::Fr*> ptabs;  // cached power tables (prove.cpp pow_table), pool-owned
     // Inside lsp_prove the host-made tree-top layers are only read by the query

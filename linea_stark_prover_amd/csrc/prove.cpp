@@ -22,11 +22,19 @@ namespace {
 // HIP events around each phase (span names as in the reference's bench.log),
 // taken from and returned to the context's event pool: creating and destroying
 // ~40 events per proof cost ~60 us of host time at the end of every proof
+// Phase events are skipped when the context's phase_timing is off
+// (lsp_ctx_set_phase_timing) or LSP_PHASE_EVENTS=0, and for phases outside
+// the context's phase_only list when it has one; lsp_last_timings reports the
+// phases that were timed
 struct PhaseTimer {
     lsp_ctx* ctx;
+    bool on;
     std::vector<std::pair<std::string, hipEvent_t>> starts;
     std::vector<std::tuple<std::string, hipEvent_t, hipEvent_t>> done;
-    explicit PhaseTimer(lsp_ctx* c) : ctx(c) {}
+    explicit PhaseTimer(lsp_ctx* c) : ctx(c) {
+        const char* e = std::getenv("LSP_PHASE_EVENTS");
+        on = c->phase_timing && !(e && *e == '0');
+    }
     hipEvent_t take() {
         hipEvent_t e;
         if (!ctx->event_pool.empty()) {
@@ -37,12 +45,21 @@ struct PhaseTimer {
         }
         return e;
     }
+    bool wanted(const std::string& name) const {
+        if (!on) return false;
+        if (ctx->phase_only.empty()) return true;
+        for (const auto& n : ctx->phase_only)
+            if (n == name) return true;
+        return false;
+    }
     void begin(const std::string& name) {
+        if (!wanted(name)) return;
         const hipEvent_t e = take();
         LSP_HIP(hipEventRecord(e, ctx->stream));
         starts.emplace_back(name, e);
     }
     void end(const std::string& name) {
+        if (!wanted(name)) return;
         for (size_t i = starts.size(); i-- > 0;) {
             if (starts[i].first == name) {
                 const hipEvent_t e = take();

@@ -99,3 +99,30 @@ def test_default_proof_is_the_in_process_proof(gpu_ctx, default_hashes):
     a, d, _ = gpu_ctx.config.seeded()
     pf = gpu_ctx.prove(gen_permutation_trace(12, 3, a, d), permutation_air(3), np.concatenate([a, d]))
     assert hashlib.sha256(pf).hexdigest() == default_hashes["12/None/None"]
+
+
+def test_phase_timing_selection(gpu_ctx):
+    """lsp_ctx_set_phase_timing: none, only the named phases, or all (the
+    default); the proof bytes do not depend on it"""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import gen_permutation_trace
+    import numpy as np
+    a, d, _ = gpu_ctx.config.seeded()
+    pub = np.concatenate([a, d])
+    air = permutation_air(3)
+    tr = gen_permutation_trace(10, 3, a, d)
+    full = gpu_ctx.prove(tr, air, pub)
+    names_all = [n for n, _ in gpu_ctx.last_timings()]
+    assert "coset_lde_batch" in names_all and "merkle tree" in names_all and "prove" in names_all
+    try:
+        gpu_ctx.set_phase_timing(False)
+        assert gpu_ctx.prove(tr, air, pub) == full
+        assert gpu_ctx.last_timings() == []
+        gpu_ctx.set_phase_timing(True, only=["coset_lde_batch", "merkle tree"])
+        assert gpu_ctx.prove(tr, air, pub) == full
+        got = gpu_ctx.last_timings()
+        assert sorted(n for n, _ in got) == ["coset_lde_batch", "merkle tree"] and all(ms > 0 for _, ms in got)
+    finally:
+        gpu_ctx.set_phase_timing(True)
+    assert gpu_ctx.prove(tr, air, pub) == full
+    assert [n for n, _ in gpu_ctx.last_timings()] == names_all

@@ -1,0 +1,134 @@
+"""Same-process A/B of two builds of liblsp_hip.so: both libraries are loaded
+side by side (distinct paths, RTLD_LOCAL), each with its own context and
+device copy of the same 2^log_n trace, and proofs alternate A, B, A, B, ...
+so both see the same clocks, the same box and the same host state.  Box-to-box
+and process-to-process noise (about 1 ms at 2^19) does not enter the paired
+differences; effects of 0.1 ms become visible.
+
+    python tools/ab_inproc.py libA.so libB.so [--log-n 19] [--pairs 30] [--env-b VAR=VAL]
+
+--env-b sets an environment variable around B's proofs only (for switches the
+library reads per call; the ones it caches at first use need two builds).
+Prints per-library median / mean / min, the median of the paired differences
+B - A and how often B won, and checks that A and B made the same proof.
+"""
+import argparse
+import ctypes
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def load(path):
+    from linea_stark_prover_amd import _lib
+    L = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL | os.RTLD_NOW)
+    for name, (res, args) in _lib._SIGS.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+class Side:
+    def __init__(self, path, log_n, ncols=3):
+        import numpy as np
+        from linea_stark_prover_amd import _lib
+        from linea_stark_prover_amd.air import permutation_air
+        from linea_stark_prover_amd.prover import StarkConfig
+        self.name = os.path.basename(path)
+        self.L = L = load(path)
+        cfg = StarkConfig()
+        a, d, rc = cfg.seeded()
+        self.rc = rc
+        self.pub = np.ascontiguousarray(np.concatenate([a, d]))
+        p = _lib.LspParams(cfg.sbox_degree, cfg.rounds_f, cfg.rounds_p, rc.ctypes.data, cfg.log_blowup,
+                           cfg.log_final_poly_len, cfg.num_queries, cfg.proof_of_work_bits, cfg.public_degree,
+                           None, None)
+        self.h = ctypes.c_void_p()
+        self._chk(L.lsp_ctx_create(0, ctypes.byref(p), ctypes.byref(self.h)))
+        self.rows, self.w = 1 << log_n, 2 * ncols + 2
+        self.dtrace = ctypes.c_void_p()
+        self._chk(L.lsp_dev_alloc(self.h, self.rows * self.w * 32, ctypes.byref(self.dtrace)))
+        self._chk(L.lsp_gen_permutation_trace_device(self.h, 1, log_n, ncols, a.ctypes.data, d.ctypes.data,
+                                                     self.dtrace))
+        desc = permutation_air(ncols).descriptor()
+        self.desc = (ctypes.c_int32 * len(desc))(*desc)
+
+    def _chk(self, rc):
+        if rc != 0:
+            msg = self.L.lsp_last_error(self.h if hasattr(self, "h") else None)
+            raise RuntimeError(f"{self.name}: lsp error {rc}: {msg.decode() if msg else ''}")
+
+    def prove(self):
+        """one proof, timed like bench.py's step (host to host), serialized"""
+        self._chk(self.L.lsp_synchronize(self.h))
+        t = time.perf_counter()
+        pf = ctypes.c_void_p()
+        self._chk(self.L.lsp_prove(self.h, self.dtrace, self.rows, self.w, self.desc, len(self.desc),
+                                   self.pub.ctypes.data, 2, 1, ctypes.byref(pf)))
+        n = ctypes.c_size_t()
+        self._chk(self.L.lsp_proof_serialize(pf, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value)
+        self._chk(self.L.lsp_proof_serialize(pf, buf, n.value, ctypes.byref(n)))
+        out = buf.raw[:n.value]
+        self.L.lsp_proof_free(pf)
+        return time.perf_counter() - t, out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("a")
+    ap.add_argument("b")
+    ap.add_argument("--log-n", type=int, default=19)
+    ap.add_argument("--pairs", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--env-b", default=None, help="VAR=VAL set around B's proofs only")
+    args = ap.parse_args()
+    A, B = Side(args.a, args.log_n), Side(args.b, args.log_n)
+    env = args.env_b.split("=", 1) if args.env_b else None
+    if env and args.a == args.b:
+        B.name += f" [{args.env_b}]"
+
+    def run_b():
+        if env:
+            old = os.environ.get(env[0])
+            os.environ[env[0]] = env[1]
+        try:
+            return B.prove()
+        finally:
+            if env:
+                if old is None:
+                    del os.environ[env[0]]
+                else:
+                    os.environ[env[0]] = old
+
+    for _ in range(args.warmup):
+        A.prove()
+        run_b()
+    ta, tb, diff = [], [], []
+    same = True
+    for i in range(args.pairs):
+        # alternate which side goes first, so a drift within a pair cancels
+        if i % 2 == 0:
+            (x, pa), (y, pb) = A.prove(), run_b()
+        else:
+            (y, pb), (x, pa) = run_b(), A.prove()
+        ta.append(x)
+        tb.append(y)
+        diff.append(y - x)
+        same = same and pa == pb
+    ms = lambda v: v * 1e3  # noqa: E731
+    for name, t in ((A.name, ta), (B.name, tb)):
+        print(f"{name:28s} median {ms(statistics.median(t)):7.2f} ms  mean {ms(statistics.mean(t)):7.2f}  "
+              f"min {ms(min(t)):7.2f}  ({len(t)} proofs, 2^{args.log_n})")
+    wins = sum(1 for d in diff if d < 0)
+    print(f"B - A: median {ms(statistics.median(diff)):+.3f} ms, mean {ms(statistics.mean(diff)):+.3f} ms; "
+          f"B faster in {wins}/{len(diff)} pairs; identical proofs: {same}")
+
+
+if __name__ == "__main__":
+    main()

@@ -16,10 +16,12 @@ for lg in logs:
     dp = ctx.dev_alloc(tr.nbytes); ctx.h2d(dp, tr)
     pf = ctx.prove(dp, air, pub, h, w)  # warm
     ts = []
-    for _ in range(3):
+    for _ in range(int(os.environ.get("LSP_TP_REPS", "3"))):
         ctx.synchronize(); t = time.time(); pf = ctx.prove(dp, air, pub, h, w); ts.append(time.time() - t)
     ok = ctx.verify(pf, air, pub)
-    print(f"log_n={lg} gen={t1-t0:.2f}s prove={min(ts)*1e3:.1f}ms rows/s={h/min(ts):.0f} verify={ok}", flush=True)
+    med = sorted(ts)[len(ts) // 2]
+    print(f"log_n={lg} gen={t1-t0:.2f}s prove={min(ts)*1e3:.1f}ms median={med*1e3:.2f}ms rows/s={h/min(ts):.0f} "
+          f"verify={ok}", flush=True)
     for name, ms in ctx.last_timings():
         print(f"   {name:55s} {ms:9.3f} ms")
     ctx.dev_free(dp)

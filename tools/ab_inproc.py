@@ -7,7 +7,7 @@ differences; effects of 0.1 ms become visible.
 
     python tools/ab_inproc.py libA.so libB.so [--log-n 19] [--pairs 30] [--env-b VAR=VAL]
 
---env-b sets an environment variable around B's proofs only (for switches the
+--env-b sets environment variables around B's proofs only (for switches the
 library reads per call; the ones it caches at first use need two builds).
 Prints per-library median / mean / min, the median of the paired differences
 B - A and how often B won, and checks that A and B made the same proof.
@@ -86,37 +86,48 @@ def main():
     ap.add_argument("--log-n", type=int, default=19)
     ap.add_argument("--pairs", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--env-b", default=None, help="VAR=VAL set around B's proofs only")
+    ap.add_argument("--env-b", default=None, help="VAR=VAL[,VAR=VAL...] set around B's proofs only")
+    ap.add_argument("--swap", action="store_true",
+                    help="one library + --env-b: apply the switch to context B, then to context A, half the pairs each")
     args = ap.parse_args()
     A, B = Side(args.a, args.log_n), Side(args.b, args.log_n)
-    env = args.env_b.split("=", 1) if args.env_b else None
-    if env and args.a == args.b:
+    envs = [kv.split("=", 1) for kv in args.env_b.split(",")] if args.env_b else []
+    if envs:
         B.name += f" [{args.env_b}]"
 
-    def run_b():
-        if env:
-            old = os.environ.get(env[0])
-            os.environ[env[0]] = env[1]
+    def with_env(side):
+        old = {k: os.environ.get(k) for k, _ in envs}
+        for k, v in envs:
+            os.environ[k] = v
         try:
-            return B.prove()
+            return side.prove()
         finally:
-            if env:
-                if old is None:
-                    del os.environ[env[0]]
+            for k, v in old.items():
+                if v is None:
+                    del os.environ[k]
                 else:
-                    os.environ[env[0]] = old
+                    os.environ[k] = v
 
     for _ in range(args.warmup):
         A.prove()
-        run_b()
+        with_env(B)
     ta, tb, diff = [], [], []
     same = True
+    # Two contexts differ by themselves (buffer placement: +-0.3 ms per 2^19
+    # proof in A/A runs).  With --swap and one library, the switch moves from
+    # context B to context A halfway, so that bias cancels in the differences.
+    swap = args.swap and args.a == args.b and envs
     for i in range(args.pairs):
+        second = swap and i >= args.pairs // 2
+        run_a = (lambda: with_env(A)) if second else A.prove
+        run_b = B.prove if second else (lambda: with_env(B))
         # alternate which side goes first, so a drift within a pair cancels
         if i % 2 == 0:
-            (x, pa), (y, pb) = A.prove(), run_b()
+            (x, pa), (y, pb) = run_a(), run_b()
         else:
-            (y, pb), (x, pa) = run_b(), A.prove()
+            (y, pb), (x, pa) = run_b(), run_a()
+        if second:
+            x, y = y, x  # x: without the switch, y: with it
         ta.append(x)
         tb.append(y)
         diff.append(y - x)

@@ -30,7 +30,7 @@ int main() {
     int bad = 0;
     for (int it = 0; it < 1000; ++it) {
         Fr a = rnd(g), b = rnd(g), c = rnd(g), x = a, y = b, z = c;
-        permute3_rt(a, b, c, rc.data(), L);
+        permute3<11>(a, b, c, rc.data(), 8, 22);
         hp64::permute3_rt(x, y, z, rc.data(), L);
         for (int j = 0; j < 8; ++j) bad += (a.v[j] != x.v[j]) + (b.v[j] != y.v[j]) + (c.v[j] != z.v[j]);
     }
@@ -39,7 +39,7 @@ int main() {
     double us[2];
     for (int v = 0; v < 2; ++v) {
         auto t = std::chrono::steady_clock::now();
-        for (int i = 0; i < N; ++i) v ? hp64::permute3_rt(s0, s1, s2, rc.data(), L) : permute3_rt(s0, s1, s2, rc.data(), L);
+        for (int i = 0; i < N; ++i) v ? hp64::permute3_rt(s0, s1, s2, rc.data(), L) : permute3<11>(s0, s1, s2, rc.data(), 8, 22);
         us[v] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t).count() / N;
     }
     printf("host permutation: generic %.2f us, 64-bit lazy %.2f us, mismatches %d (%08x)\n", us[0], us[1], bad, s0.v[0]);

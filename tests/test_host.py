@@ -216,3 +216,15 @@ def test_fold_row_host_matches_pyoracle(product_lib):
             b, e0, e1 = rng.sample_fr(), rng.sample_fr(), rng.sample_fr()
             got = TwoAdicFriGenericConfig.fold_row(idx, logh, to_mont([b]), to_mont([e0]), to_mont([e1]))
             assert from_mont(got)[0] == O.fold_row(idx, logh, b, e0, e1)
+
+
+def test_phase_timing_arguments(host_ctx, product_lib):
+    """lsp_ctx_set_phase_timing validates its arguments (no GPU needed to set it)"""
+    from linea_stark_prover_amd import _lib
+    names = (ctypes.c_char_p * 2)(b"coset_lde_batch", None)
+    assert product_lib.lsp_ctx_set_phase_timing(None, 1, None, 0) == _lib.LSP_E_ARG
+    assert product_lib.lsp_ctx_set_phase_timing(host_ctx.h, 1, None, 1) == _lib.LSP_E_ARG   # n_only > 0, no list
+    assert product_lib.lsp_ctx_set_phase_timing(host_ctx.h, 1, names, 2) == _lib.LSP_E_ARG  # a null name
+    assert product_lib.lsp_ctx_set_phase_timing(host_ctx.h, 1, names, 1) == _lib.LSP_OK
+    host_ctx.set_phase_timing(False)
+    host_ctx.set_phase_timing(True)

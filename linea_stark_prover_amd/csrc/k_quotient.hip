@@ -8,6 +8,8 @@
 // constraint order of eval.  Row `local` is LDE row bitrev_Q(i) and `next`
 // is bitrev_Q((i + 2^log_q) mod Q) (get_evaluations_on_domain +
 // vertically_packed_row_pair).
+#include <cstdlib>
+
 #include "fr29.hpp"
 #include "k_common.hpp"
 #include "kernels.hpp"
@@ -58,14 +60,15 @@ __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
     const size_t t = gtid();
     const size_t Q = 1ull << a.logQ;
     if (t >= (a.n ? a.n : Q)) return;  // n = Q >> log_step points
-    // Wide rows: thread t evaluates point m = bitrev(t), whose row bitrev_Q(i)
+    // Row order: thread t evaluates point m = bitrev(t), whose row bitrev_Q(i)
     // is row0 + t, so a wave reads 64 adjacent LDE rows (and their
-    // successors).  In point order it read rows Q/64 apart, and with the C3
+    // successors).  In point order it read rows Q/64 apart: with the C3
     // trace's 5.9 KB rows their lines left the L2 before the lane came back
-    // for the next columns (2^20 x 184: 63.5 -> 36.7 ms).  Narrow rows keep
-    // point order (coalesced inv_den reads and out writes; 2^19 x 8 is ~5 %
-    // faster that way).
-    const size_t m = a.w >= 32 ? brev_bits(t, a.logQ - a.log_step) : t;
+    // for the next columns (2^20 x 184: 63.5 -> 36.7 ms), and with narrow
+    // rows past the caches' size every row is a DRAM page miss (round 3:
+    // 2^22 x 8 5.7 -> 3.9 ms).  Point order (coalesced inv_den reads and out
+    // writes) remains for A/B runs (row_order = 0).
+    const size_t m = a.row_order ? brev_bits(t, a.logQ - a.log_step) : t;
     const uint64_t i = a.i0 + ((uint64_t)m << a.log_step);
     const uint32_t qmask = (1u << a.log_q) - 1;
     const F29 one = f29_from_fr(fr_one());
@@ -149,9 +152,20 @@ hipError_t launch_selector_denoms(const Fr* tabQ, uint32_t L1, Fr gen, Fr wh_inv
     return hipGetLastError();
 }
 
+// Thread order: LDE row order (LSP_QUOTIENT_ORDER=point: point order; read per
+// call).  Row order measured faster at every size (profiles/r03x_quotient_order.txt:
+// 2^19 x 8 0.475 -> 0.45 ms, 2^22 x 8 5.7 -> 3.9 ms, rank 0 of 2^26 over 8 ranks
+// 60 -> 26 ms): in point order a wave's 64 rows are Q/64 apart, and past the
+// caches' size every row is a DRAM page miss.
 hipError_t launch_quotient(const QuotientArgs& a, hipStream_t st) {
     const size_t n = a.n ? a.n : (1ull << a.logQ);
-    hipLaunchKernelGGL(k_quotient, dim3(nblocks(n, 256)), dim3(256), 0, st, a);
+    QuotientArgs b = a;
+    b.row_order = 1;
+    if (const char* e = std::getenv("LSP_QUOTIENT_ORDER")) {
+        if (e[0] == 'r') b.row_order = 1;
+        if (e[0] == 'p') b.row_order = 0;
+    }
+    hipLaunchKernelGGL(k_quotient, dim3(nblocks(n, 256)), dim3(256), 0, st, b);
     return hipGetLastError();
 }
 

@@ -195,6 +195,9 @@ struct QuotientArgs {
     // nullptr: in `lde` (every point's successor on the same rank)
     const Fr* lde_next = nullptr;
     uint64_t row0_next = 0;
+    // thread order (launch_quotient sets it; LSP_QUOTIENT_ORDER): 1 = LDE row
+    // order (a wave reads 64 adjacent rows, the default), 0 = point order
+    uint32_t row_order = 0;
 };
 // den[m] = (x_i - 1)(x_i - w_h^-1), x_i = GEN * w_Q^i, i = i0 + (m << log_step), m < n
 hipError_t launch_selector_denoms(const Fr* tabQ, uint32_t L1, Fr gen, Fr wh_inv, size_t n, Fr* den,

@@ -115,25 +115,34 @@ int lsp_seeded_setup(uint64_t seed, uint32_t rounds_f, uint32_t rounds_p, lsp_fr
     });
 }
 
+// The scalar helpers return nothing (the reference's field methods cannot
+// fail); a null argument makes them a no-op instead of a fault.
 void lsp_fr_from_canonical(const uint64_t in[4], lsp_fr* out) {
+    if (!in || !out) return;
     lsp_fr t;
     std::memcpy(t.l, in, 32);
     *out = from_fr(fr_from_canonical(to_fr(t)));
 }
 void lsp_fr_to_canonical(const lsp_fr* in, uint64_t out[4]) {
+    if (!in || !out) return;
     lsp_fr t = from_fr(fr_to_canonical(to_fr(*in)));
     std::memcpy(out, t.l, 32);
 }
 void lsp_fr_from_be_bytes_mod_order(const uint8_t* be, size_t n, lsp_fr* out) {
+    if (!out || (!be && n)) return;
     // Horner over bytes: acc = acc * 256 + byte (mod r)
     const Fr b256 = fr_from_u64(256);
     Fr acc = fr_zero();
     for (size_t i = 0; i < n; ++i) acc = fr_add(fr_mul(acc, b256), fr_from_u64(be[i]));
     *out = from_fr(acc);
 }
-void lsp_fr_mul(const lsp_fr* a, const lsp_fr* b, lsp_fr* out) { *out = from_fr(fr_mul(to_fr(*a), to_fr(*b))); }
-void lsp_fr_inv(const lsp_fr* a, lsp_fr* out) { *out = from_fr(fr_inv(to_fr(*a))); }
+void lsp_fr_mul(const lsp_fr* a, const lsp_fr* b, lsp_fr* out) {
+    if (a && b && out) *out = from_fr(fr_mul(to_fr(*a), to_fr(*b))); }
+void lsp_fr_inv(const lsp_fr* a, lsp_fr* out) {
+    if (a && out) *out = from_fr(fr_inv(to_fr(*a)));
+}
 void lsp_two_adic_generator(uint32_t bits, lsp_fr* out) {
+    if (!out) return;
     if (bits > 47) bits = 47;
     *out = from_fr(host_two_adic_generator(bits));
 }
@@ -253,16 +262,25 @@ int lsp_dev_alloc(lsp_ctx* ctx, size_t bytes, void** dptr) {
     });
 }
 int lsp_dev_free(lsp_ctx* ctx, void* dptr) {
-    return guarded(ctx, [&] { LSP_HIP(hipFree(dptr)); });
+    return guarded(ctx, [&] {
+        need_gpu(ctx);
+        LSP_HIP(hipFree(dptr));
+    });
 }
 int lsp_memcpy_h2d(lsp_ctx* ctx, void* dst, const void* src, size_t bytes) {
     return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && ((dst && src) || bytes == 0), LSP_E_ARG, "null memcpy argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
         LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
         ctx->sync();
     });
 }
 int lsp_memcpy_d2h(lsp_ctx* ctx, void* dst, const void* src, size_t bytes) {
     return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && ((dst && src) || bytes == 0), LSP_E_ARG, "null memcpy argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
         LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
         ctx->sync();
     });
@@ -451,6 +469,7 @@ int lsp_fri_fold(lsp_ctx* ctx, const lsp_fr* v, size_t len, const lsp_fr* beta, 
 
 void lsp_fri_fold_row(size_t index, uint32_t log_height, const lsp_fr* beta, const lsp_fr* e0, const lsp_fr* e1,
                       lsp_fr* out) {
+    if (!beta || !e0 || !e1 || !out) return;
     const Fr s0 = fr_pow_u64(host_two_adic_generator(log_height + 1), host_bitrev(index, log_height));
     const Fr a = to_fr(*e0), b = to_fr(*e1);
     const Fr r = fr_add(a, fr_mul(fr_mul(fr_sub(to_fr(*beta), s0), fr_sub(b, a)), fr_inv(fr_sub(fr_neg(s0), s0))));
@@ -977,7 +996,7 @@ int lsp_last_spans(const lsp_ctx* ctx, const char** lines, size_t cap, size_t* n
 
 int lsp_calibrate_fr_mul(lsp_ctx* ctx, double* gmul_per_s) {
     return guarded(ctx, [&] {
-        LSP_REQUIRE(gmul_per_s, LSP_E_ARG, "null");
+        LSP_REQUIRE(ctx && gmul_per_s, LSP_E_ARG, "null");
         std::lock_guard<std::mutex> g(ctx->mu);
         need_gpu(ctx);
         const size_t nth = 256 * 256 * 16;  // 16 blocks of 256 lanes per CU
@@ -1149,7 +1168,7 @@ int lsp_raw_trace_free(lsp_raw_trace* t) {
 
 int lsp_calibrate_poseidon2(lsp_ctx* ctx, double* mperm_per_s) {
     return guarded(ctx, [&] {
-        LSP_REQUIRE(mperm_per_s, LSP_E_ARG, "null");
+        LSP_REQUIRE(ctx && mperm_per_s, LSP_E_ARG, "null");
         std::lock_guard<std::mutex> g(ctx->mu);
         need_gpu(ctx);
         // the peak: best of several grid sizes (2..32 blocks of 256 lanes per CU)

@@ -106,7 +106,10 @@ int lsp_seeded_setup(uint64_t seed, uint32_t rounds_f, uint32_t rounds_p, lsp_fr
                      lsp_fr *round_constants);
 
 /* Field conversions (host).  from_be_bytes_mod_order replaces
- * FF_Bls12_377Fr::from_be_bytes_mod_order (trace/src/permutation.rs:102-104). */
+ * FF_Bls12_377Fr::from_be_bytes_mod_order (trace/src/permutation.rs:102-104).
+ * These helpers (and lsp_fri_fold_row) return nothing; a NULL argument makes
+ * them a no-op.  Every int-returning entry point reports NULL arguments as
+ * LSP_E_ARG (tests/test_abi_sweep.py). */
 void lsp_fr_from_canonical(const uint64_t in[4], lsp_fr *out);
 void lsp_fr_to_canonical(const lsp_fr *in, uint64_t out[4]);
 void lsp_fr_from_be_bytes_mod_order(const uint8_t *be, size_t n, lsp_fr *out);

@@ -141,6 +141,20 @@ int lsp_coset_lde_batch(lsp_ctx *ctx, const lsp_fr *in, size_t h, size_t w, uint
  * where chunk j uses GEN / (GEN * w_Q^j)). */
 int lsp_coset_lde_batch_shifts(lsp_ctx *ctx, const lsp_fr *in, size_t h, size_t w, uint32_t added_bits,
                                const lsp_fr *shifts, lsp_fr *out, int mem);
+/* The rest of the TwoAdicSubgroupDft surface ([EXT p3-dft]; Radix2DitParallel
+ * is the reference's Dft, bin/src/config.rs:22), h = 2^k >= 1, w >= 1:
+ * coset_dft_batch(mat, shift) (dft_batch: shift = NULL, i.e. 1):
+ *   coeffs: h x w true coefficients, row i = c_i; out: h x w evaluations on
+ *   shift * H_h stored bit-reversed, row j = p(shift * w_h^bitrev(j)) -- the
+ *   Evaluations = BitReversedMatrixView layout Radix2DitParallel returns.
+ * coset_idft_batch(mat, shift) (idft_batch: shift = NULL):
+ *   evals: h x w natural order, row i = p(shift * w_h^i); out: h x w
+ *   coefficients, canonical.  shift must be nonzero.
+ * lde_batch(mat, added_bits) is lsp_coset_lde_batch with shift 1. */
+int lsp_coset_dft_batch(lsp_ctx *ctx, const lsp_fr *coeffs, size_t h, size_t w, const lsp_fr *shift, lsp_fr *out,
+                        int mem);
+int lsp_coset_idft_batch(lsp_ctx *ctx, const lsp_fr *evals, size_t h, size_t w, const lsp_fr *shift, lsp_fr *out,
+                         int mem);
 
 /* ---------------------------------------------------- Poseidon2 / symmetric */
 /* Poseidon2Bls12337<3>::permute_mut on n states of 3 (bin/src/config.rs:11) */

@@ -65,6 +65,10 @@ _SIGS = {
                                            ctypes.c_uint32, c_fr_p, c_fr_p, ctypes.c_int]),
     "lsp_coset_lde_batch_shifts": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t,
                                                   ctypes.c_uint32, c_fr_p, c_fr_p, ctypes.c_int]),
+    "lsp_coset_dft_batch": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, c_fr_p, c_fr_p,
+                                           ctypes.c_int]),
+    "lsp_coset_idft_batch": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, c_fr_p, c_fr_p,
+                                            ctypes.c_int]),
     "lsp_poseidon2_permute_batch": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_int]),
     "lsp_hash_rows": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, c_fr_p,
                                      ctypes.c_int]),

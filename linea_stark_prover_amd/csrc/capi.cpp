@@ -311,6 +311,37 @@ int lsp_coset_lde_batch(lsp_ctx* ctx, const lsp_fr* in, size_t h, size_t w, uint
     return lsp_coset_lde_batch_shifts(ctx, in, h, w, added_bits, sh.data(), out, mem);
 }
 
+int lsp_coset_dft_batch(lsp_ctx* ctx, const lsp_fr* coeffs, size_t h, size_t w, const lsp_fr* shift, lsp_fr* out,
+                        int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && w >= 1, LSP_E_ARG, "bad dft arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        log2_exact(h);
+        const Fr s = shift ? to_fr(*shift) : fr_one();
+        const Fr* din = dev_in(ctx, coeffs, h * w, mem, "api_in");
+        Fr* dout = dev_out(ctx, out, h * w, mem, "api_out");
+        coset_dft_device(ctx, din, h, w, s, dout);
+        finish_out(ctx, out, dout, h * w, mem);
+    });
+}
+
+int lsp_coset_idft_batch(lsp_ctx* ctx, const lsp_fr* evals, size_t h, size_t w, const lsp_fr* shift, lsp_fr* out,
+                         int mem) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && w >= 1, LSP_E_ARG, "bad idft arguments");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        log2_exact(h);
+        const Fr s = shift ? to_fr(*shift) : fr_one();
+        LSP_REQUIRE(!fr_is_zero(fr_to_canonical(s)), LSP_E_ARG, "coset shift must be nonzero");
+        const Fr* din = dev_in(ctx, evals, h * w, mem, "api_in");
+        Fr* dout = dev_out(ctx, out, h * w, mem, "api_out");
+        coset_idft_device(ctx, din, h, w, s, dout);
+        finish_out(ctx, out, dout, h * w, mem);
+    });
+}
+
 int lsp_poseidon2_permute_batch(lsp_ctx* ctx, lsp_fr* states, size_t n, int mem) {
     return guarded(ctx, [&] {
         LSP_REQUIRE(ctx, LSP_E_ARG, "null ctx");

@@ -534,6 +534,17 @@ __global__ __launch_bounds__(256) void k_fold_subcoset(const Fr* __restrict__ co
     out[e] = f29_store(acc, false);
 }
 
+// out[i][c] = X[i][c] f^i canonical, f^i from a two-level table of 29-bit-form
+// factors (pow2l29): the coefficients of an inverse transform (h * c_i, as
+// launch_intt leaves them) times (1/h) shift^-i (coset_idft_batch)
+__global__ __launch_bounds__(256) void k_scale_coeffs(const Fr* __restrict__ X, size_t h, uint32_t w,
+                                                      const Fr* __restrict__ tab, uint32_t L1, Fr* __restrict__ out) {
+    const size_t e = gtid();
+    if (e >= h * w) return;
+    const size_t i = e / w;
+    out[e] = f29_store(f29_reduce(f29_mul(f29_repack_in(X[e]), pow2l29(tab, L1, i))), true);
+}
+
 // ark-form words -> the 29-bit Montgomery form x 2^261 mod r, canonical, packed
 // in 8 words (twiddle and twist tables of k_ntt_rm)
 __global__ __launch_bounds__(256) void k_to_f29form(const Fr* __restrict__ in, Fr* __restrict__ out, size_t n) {
@@ -763,6 +774,13 @@ hipError_t launch_fold_subcoset(const Fr* coef, ColMap map, size_t h, size_t S, 
     if (S == 0 || h % S != 0 || h / S > 64 || w == 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_fold_subcoset, dim3(nblocks(S * w, 256)), dim3(256), 0, st, coef, map, (uint64_t)h,
                        (uint64_t)S, w, (uint32_t)(h / S), fac, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_scale_coeffs(const Fr* X, size_t h, uint32_t w, const Fr* tab, uint32_t L1, Fr* out,
+                               hipStream_t st) {
+    if (h * w == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scale_coeffs, dim3(nblocks(h * w, 256)), dim3(256), 0, st, X, h, w, tab, L1, out);
     return hipGetLastError();
 }
 

@@ -68,6 +68,9 @@ hipError_t launch_fold_subcoset(const Fr* coef, ColMap map, size_t h, size_t S, 
                                 hipStream_t st);
 // ark-form words -> the 29-bit Montgomery form (x 2^261 mod r), canonical, in place allowed
 hipError_t launch_to_f29form(const Fr* in, Fr* out, size_t n, hipStream_t st);
+// out[i][c] = X[i][c] * f^i, canonical; tab: two-level table of f in the 29-bit form (k_scale_coeffs)
+hipError_t launch_scale_coeffs(const Fr* X, size_t h, uint32_t w, const Fr* tab, uint32_t L1, Fr* out,
+                               hipStream_t st);
 // the same, unpacked into 9 x 29-bit limbs padded to 48 bytes (3 x uint4 per
 // element): the NTT's twiddle tables, loaded with no repacking
 hipError_t launch_to_f29limbs(const Fr* in, uint4* out, size_t n, hipStream_t st);

@@ -135,14 +135,15 @@ Fr d2h_fr(lsp_ctx* ctx, const Fr* d) {
 // ----------------------------------------------------------------- LDE
 // The twist tables of coset blocks [k0, k0 + nk) of an h x w LDE: coset k,
 // column c has base s = shift_c * w_N^bitrev(k); coefficient i is scaled by
-// s^i / h.  Built once per (log h, cosets, shifts) and kept in the context.
+// s^i / h (s^i with div_h false: a transform of true coefficients).  Built
+// once per (log h, cosets, shifts, div_h) and kept in the context.
 struct TwistTables {
     const Fr* tabs;
     uint32_t L1, L2;
     bool shared;  // one table per coset (every column's shift is the same)
 };
 static TwistTables lde_twist(lsp_ctx* ctx, size_t h, size_t w, uint32_t added_bits, const Fr* shifts_host, uint32_t k0,
-                             uint32_t nk) {
+                             uint32_t nk, bool div_h = true) {
     const uint32_t logh = log2_exact(h);
     const uint32_t logN = logh + added_bits;
     hipStream_t st = ctx->stream;
@@ -157,16 +158,16 @@ static TwistTables lde_twist(lsp_ctx* ctx, size_t h, size_t w, uint32_t added_bi
     for (size_t c = 0; c < per_coset; ++c)
         for (int i = 0; i < 8; ++i) hsh = (hsh ^ shifts_host[c].v[i]) * 1099511628211ull;
     char key[112];
-    std::snprintf(key, sizeof key, "ldetw_%u_%u_%u_%u_%zu_%016llx", logh, added_bits, k0, nk, per_coset,
-                  (unsigned long long)hsh);
+    std::snprintf(key, sizeof key, "ldetw_%u_%u_%u_%u_%zu_%d_%016llx", logh, added_bits, k0, nk, per_coset,
+                  div_h ? 1 : 0, (unsigned long long)hsh);
     auto it = ctx->ptabs.find(key);
     if (it != ctx->ptabs.end()) {
         T.tabs = it->second;
         return T;
     }
     const Fr wN = host_two_adic_generator(logN);
-    const Fr hinv = host_inv_cached(fr_from_u64(h));
-    std::vector<Fr> bases(2 * nb, hinv);  // nb bases, then nb scales (1/h)
+    const Fr hinv = div_h ? host_inv_cached(fr_from_u64(h)) : fr_one();
+    std::vector<Fr> bases(2 * nb, hinv);  // nb bases, then nb scales (1/h or 1)
     for (uint32_t k = 0; k < nk; ++k) {
         const Fr ck = fr_pow_u64(wN, host_bitrev(k0 + k, added_bits));
         for (size_t c = 0; c < per_coset; ++c) bases[k * per_coset + c] = fr_mul(shifts_host[c], ck);
@@ -201,12 +202,55 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
 // The same blocks from h * coefficients (natural order) at `coef`, laid out
 // as `map` says -- the forward half, for ranks that split the inverse
 static void lde_coeffs_device(lsp_ctx* ctx, const Fr* coef, ColMap map, size_t h, size_t w, uint32_t added_bits,
-                              const Fr* shifts_host, Fr* d_out, uint32_t k0, uint32_t nk) {
+                              const Fr* shifts_host, Fr* d_out, uint32_t k0, uint32_t nk, bool div_h = true) {
     const uint32_t logh = log2_exact(h);
     LSP_REQUIRE(k0 + nk <= (1u << added_bits) && logh >= 1, LSP_E_ARG, "coset range outside the LDE");
-    const TwistTables T = lde_twist(ctx, h, w, added_bits, shifts_host, k0, nk);
+    const TwistTables T = lde_twist(ctx, h, w, added_bits, shifts_host, k0, nk, div_h);
     LSP_HIP(launch_lde_coeffs(coef, map, d_out, w, logh, nk, ctx->twiddle29(logh, false), T.tabs, T.L1, T.L2,
                               T.shared ? 0 : 1, ctx->stream));
+}
+
+// TwoAdicSubgroupDft::coset_dft_batch ([EXT p3-dft]; dft_batch: shift 1): the
+// h x w true coefficients at d_coef -> evaluations on shift H_h, stored
+// bit-reversed (row j = p(shift w_h^bitrev(j)), Radix2DitParallel's
+// Evaluations layout) -- the forward half of the LDE with one block and
+// twist s^i instead of s^i / h
+void coset_dft_device(lsp_ctx* ctx, const Fr* d_coef, size_t h, size_t w, const Fr& shift, Fr* d_out) {
+    const uint32_t logh = log2_exact(h);
+    LSP_REQUIRE(logh <= 40, LSP_E_SIZE, "transform too large");
+    if (h == 1) {  // p(x) = c_0 everywhere
+        if (d_out != d_coef)
+            LSP_HIP(hipMemcpyAsync(d_out, d_coef, w * sizeof(Fr), hipMemcpyDeviceToDevice, ctx->stream));
+        return;
+    }
+    const std::vector<Fr> sh(w, shift);
+    lde_coeffs_device(ctx, d_coef, ColMap::plain((uint32_t)w), h, w, 0, sh.data(), d_out, 0, 1, false);
+}
+
+// TwoAdicSubgroupDft::coset_idft_batch (idft_batch: shift 1): evaluations on
+// shift H_h in natural row order -> the coefficients (natural order,
+// canonical): the LDE's inverse half (h c_i), then c_i = X_i (1/h) shift^-i
+void coset_idft_device(lsp_ctx* ctx, const Fr* d_evals, size_t h, size_t w, const Fr& shift, Fr* d_out) {
+    const uint32_t logh = log2_exact(h);
+    LSP_REQUIRE(logh <= 40, LSP_E_SIZE, "transform too large");
+    LSP_REQUIRE(!fr_is_zero(fr_to_canonical(shift)), LSP_E_ARG, "coset shift must be nonzero");
+    uint32_t L1, L2;
+    two_level(logh, L1, L2);
+    const size_t per = (1ull << L1) + (1ull << L2);
+    Fr* tab = ctx->fbuf("idft_tab", per);
+    Fr* b = ctx->fbuf("idft_tab_base", 2);
+    const Fr base_scale[2] = {host_inv_cached(shift), host_inv_cached(fr_from_u64(h))};
+    LSP_HIP(hipMemcpyAsync(b, base_scale, sizeof base_scale, hipMemcpyHostToDevice, ctx->stream));
+    LSP_HIP(launch_pow_tables(b, 1, L1, L2, b + 1, tab, ctx->stream));
+    LSP_HIP(launch_to_f29form(tab, tab, per, ctx->stream));
+    const Fr* X = d_evals;  // h = 1: the value is the coefficient
+    if (h > 1) {
+        Fr* x = ctx->fbuf("idft_X", h * w);
+        LSP_HIP(launch_intt(d_evals, ColMap::plain((uint32_t)w), x, w, logh, ctx->twiddle29(logh, true), ctx->stream));
+        X = x;
+    }
+    LSP_HIP(launch_scale_coeffs(X, h, (uint32_t)w, tab, L1, d_out, ctx->stream));
+    LSP_HIP(hipStreamSynchronize(ctx->stream));  // `base_scale` is a host temporary
 }
 
 // Block `blk` (S = N / 2^b rows, S < h) of the bit-reversed N-row LDE, when a

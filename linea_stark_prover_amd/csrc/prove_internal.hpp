@@ -8,6 +8,10 @@ namespace lsp {
 // with nk > 0 only the coset blocks [k0, k0 + nk) (rows k0*h .. (k0+nk)*h - 1 of the full result)
 void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added_bits, const Fr* shifts_host,
                 Fr* d_out, uint32_t k0 = 0, uint32_t nk = 0);
+// TwoAdicSubgroupDft::coset_dft_batch / coset_idft_batch on device matrices (h x w row-major):
+// coefficients -> evaluations on shift H_h stored bit-reversed, and natural-order evaluations -> coefficients
+void coset_dft_device(lsp_ctx* ctx, const Fr* d_coef, size_t h, size_t w, const Fr& shift, Fr* d_out);
+void coset_idft_device(lsp_ctx* ctx, const Fr* d_evals, size_t h, size_t w, const Fr& shift, Fr* d_out);
 // leaves + every layer into `layers` (2*height - 1); returns the root
 // fold: when set, the leaves are the pairs of the FRI fold it describes (fused
 // into the leaf kernel; m.ptr[0] receives the folded vector)

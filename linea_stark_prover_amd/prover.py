@@ -153,6 +153,28 @@ class Context:
                                                          L.LSP_MEM_HOST))
         return out
 
+    def coset_dft_batch(self, coeffs: np.ndarray, shift=None) -> np.ndarray:
+        """TwoAdicSubgroupDft::coset_dft_batch (dft_batch: shift None): h x w
+        coefficients -> evaluations on shift*H_h, rows bit-reversed"""
+        coeffs = _fr_arr(coeffs)
+        h, w = coeffs.shape[0], coeffs.shape[1]
+        out = np.zeros((h, w, 4), np.uint64)
+        sh = None if shift is None else _fr_arr(shift).reshape(4)
+        self._chk(L.lib().lsp_coset_dft_batch(self.h, _ptr(coeffs), h, w, None if sh is None else _ptr(sh), _ptr(out),
+                                              L.LSP_MEM_HOST))
+        return out
+
+    def coset_idft_batch(self, evals: np.ndarray, shift=None) -> np.ndarray:
+        """TwoAdicSubgroupDft::coset_idft_batch (idft_batch: shift None): h x w
+        evaluations on shift*H_h in natural order -> coefficients"""
+        evals = _fr_arr(evals)
+        h, w = evals.shape[0], evals.shape[1]
+        out = np.zeros((h, w, 4), np.uint64)
+        sh = None if shift is None else _fr_arr(shift).reshape(4)
+        self._chk(L.lib().lsp_coset_idft_batch(self.h, _ptr(evals), h, w, None if sh is None else _ptr(sh), _ptr(out),
+                                               L.LSP_MEM_HOST))
+        return out
+
     # -------------------------------------------------------------- symmetric
     def poseidon2_permute(self, states: np.ndarray) -> np.ndarray:
         s = _fr_arr(states).copy()
@@ -313,6 +335,22 @@ class Radix2DitParallel:
 
     def coset_lde_batch(self, mat: np.ndarray, added_bits: int, shift) -> np.ndarray:
         return self.ctx.coset_lde_batch(mat, added_bits, shift)
+
+    def lde_batch(self, mat: np.ndarray, added_bits: int) -> np.ndarray:
+        from .field import to_mont
+        return self.ctx.coset_lde_batch(mat, added_bits, to_mont([1])[0])
+
+    def dft_batch(self, coeffs: np.ndarray) -> np.ndarray:
+        return self.ctx.coset_dft_batch(coeffs)
+
+    def coset_dft_batch(self, coeffs: np.ndarray, shift) -> np.ndarray:
+        return self.ctx.coset_dft_batch(coeffs, shift)
+
+    def idft_batch(self, evals: np.ndarray) -> np.ndarray:
+        return self.ctx.coset_idft_batch(evals)
+
+    def coset_idft_batch(self, evals: np.ndarray, shift) -> np.ndarray:
+        return self.ctx.coset_idft_batch(evals, shift)
 
 
 class MerkleTree:

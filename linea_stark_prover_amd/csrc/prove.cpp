@@ -634,7 +634,7 @@ static Fr shard_root(lsp_ctx* ctx, Comm& comm, const Fr& local, std::vector<std:
 // (G <= blowup), hence a whole subtree of every input Merkle tree, the
 // quotient points whose rows it holds, and a contiguous slice of every FRI
 // vector.  Exchanges: subtree roots, the quotient chunks (one allgather),
-// the opened values (broadcast from rank 0, which holds the low coset), the
+// the opened values (each computed on one rank's first coset, allgathered), the
 // FRI vector once a slice is shorter than FRI_SHARD_MIN, and the query
 // openings.  The transcript runs on every rank with identical inputs.
 lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, size_t w, const Air& air,
@@ -897,46 +897,64 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         }
         T.end("compute_inverse_denominators");
         T.begin("compute opened values with Lagrange interpolation");
-        // barycentric sums on the low coset (first h rows: rank 0), then the host-side factor
+        // Barycentric sums over one coset c H_h of the LDE domain: p(z) =
+        // (z^h - c^h) / (h c^h) * sum_i p(x_i) x_i / (z - x_i).  Any coset gives
+        // the same (unique) value, so with whole cosets per rank the three jobs
+        // (trace at zeta, trace at zeta*w_h, the chunks at zeta) go to the ranks
+        // that evaluated no quotient points (g >= Gq), each over its first coset,
+        // instead of all to rank 0; an allgather of the values replaces rank 0's
+        // broadcast.  sub: the low coset's h / S ranks add partial sums.
         const size_t maxw = std::max(w, q);
-        Fr* sums = ctx->fbuf("o_sums", 2 * w + q);
-        const size_t nlow = std::min(S, h);  // this rank's rows of the low coset (sub: ranks 0 .. h/S - 1)
-        if (row0 < h) {
-            Fr* partial = ctx->fbuf("o_partial", ((nlow + 1023) / 1024) * maxw);
-            uint32_t nb = 0;
-            LSP_HIP(launch_interp_partial(lde, (uint32_t)w, nlow, inv_z, GEN, tabN, L1N, logN, partial, &nb, st, row0));
-            LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)w, sums, st));
-            LSP_HIP(launch_interp_partial(lde, (uint32_t)w, nlow, inv_zn, GEN, tabN, L1N, logN, partial, &nb, st, row0));
-            LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)w, sums + w, st));
-            LSP_HIP(launch_interp_partial(qlde, (uint32_t)q, nlow, inv_z, GEN, tabN, L1N, logN, partial, &nb, st, row0));
-            LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)q, sums + 2 * w, st));
-        } else if (sub) {
-            LSP_HIP(hipMemsetAsync(sums, 0, (2 * w + q) * sizeof(Fr), st));
+        const size_t nsum = 2 * w + q;
+        Fr* sums = ctx->fbuf("o_sums", nsum);
+        const size_t nlow = std::min(S, h);  // this rank's rows of one coset
+        const size_t joff[3] = {0, w, 2 * w}, jw[3] = {w, w, q};
+        bool job_here[3] = {false, false, false};
+        if (sub) {
+            job_here[0] = job_here[1] = job_here[2] = row0 < h;  // ranks 0 .. h/S - 1: the low coset's partial sums
+        } else {
+            const uint32_t nfree = G > Gq ? (uint32_t)(G - Gq) : 0u;
+            for (int j = 0; j < 3; ++j)
+                job_here[j] = g == (nfree ? G - 1 - (uint32_t)j % nfree : G - 1 - (uint32_t)j % G);
         }
-        if (G > 1 && !sub) comm.bcast(ctx, sums, (2 * w + q) * sizeof(Fr), 0);
-        Fr* hs = (Fr*)ctx->hbuf("o_sums_h", (2 * w + q) * sizeof(Fr));  // pinned
-        LSP_HIP(hipMemcpyAsync(hs, sums, (2 * w + q) * sizeof(Fr), hipMemcpyDeviceToHost, st));
-        LSP_HIP(hipStreamSynchronize(st));
-        if (sub) {  // the low coset's partial sums from its h / S ranks
-            const std::vector<Fr> all = comm.allgather_fr(ctx, hs, 2 * w + q);
-            for (size_t k = 0; k < 2 * w + q; ++k) {
+        if (job_here[0] || job_here[1] || job_here[2]) {
+            Fr* partial = ctx->fbuf("o_partial", ((nlow + 1023) / 1024) * maxw);
+            const Fr* jm[3] = {lde, lde, qlde};
+            const Fr* jinv[3] = {inv_z, inv_zn, inv_z};
+            for (int j = 0; j < 3; ++j) {
+                if (!job_here[j]) continue;
+                uint32_t nb = 0;
+                LSP_HIP(launch_interp_partial(jm[j], (uint32_t)jw[j], nlow, jinv[j], GEN, tabN, L1N, logN, partial, &nb,
+                                              st, row0));
+                LSP_HIP(launch_sum_partials(partial, nb, (uint32_t)jw[j], sums + joff[j], st));
+            }
+        }
+        Fr* hs = (Fr*)ctx->hbuf("o_sums_h", nsum * sizeof(Fr));  // pinned
+        if (job_here[0] || job_here[1] || job_here[2]) {
+            LSP_HIP(hipMemcpyAsync(hs, sums, nsum * sizeof(Fr), hipMemcpyDeviceToHost, st));
+            LSP_HIP(hipStreamSynchronize(st));
+        }
+        // the coset of this rank's first rows: c = GEN w_N^bitrev(row0) (sub: the low coset, GEN)
+        const Fr cpos = sub ? GEN : fr_mul(GEN, fr_pow_u64(host_two_adic_generator(logN), host_bitrev(row0, logN)));
+        const Fr ch_ = fr_pow_u64(cpos, h);
+        const Fr dinv = host_inv_cached(fr_mul(ch_, fr_from_u64(h)));
+        auto factor = [&](const Fr& z) { return fr_mul(fr_sub(fr_pow_u64(z, h), ch_), dinv); };
+        const Fr jz[3] = {zeta, zeta_next, zeta};
+        for (int j = 0; j < 3; ++j) {
+            const Fr f = factor(jz[j]);
+            for (size_t k = 0; k < jw[j]; ++k) hs[joff[j] + k] = job_here[j] ? fr_mul(hs[joff[j] + k], f) : fr_zero();
+        }
+        if (G > 1) {  // every value from its job's rank(s): the sum over ranks
+            const std::vector<Fr> all = comm.allgather_fr(ctx, hs, nsum);
+            for (size_t k = 0; k < nsum; ++k) {
                 Fr acc = fr_zero();
-                for (uint32_t r = 0; r < G; ++r) acc = fr_add(acc, all[(size_t)r * (2 * w + q) + k]);
+                for (uint32_t r = 0; r < G; ++r) acc = fr_add(acc, all[(size_t)r * nsum + k]);
                 hs[k] = acc;
             }
         }
-        const Fr gh = fr_pow_u64(GEN, h);
-        const Fr dinv = host_inv_cached(fr_mul(gh, fr_from_u64(h)));
-        auto factor = [&](const Fr& z) { return fr_mul(fr_sub(fr_pow_u64(z, h), gh), dinv); };
-        const Fr fz = factor(zeta), fzn = factor(zeta_next);
-        proof->tl.resize(w);
-        proof->tn.resize(w);
-        proof->qc.resize(q);
-        for (size_t c = 0; c < w; ++c) {
-            proof->tl[c] = fr_mul(hs[c], fz);
-            proof->tn[c] = fr_mul(hs[w + c], fzn);
-        }
-        for (size_t j = 0; j < q; ++j) proof->qc[j] = fr_mul(hs[2 * w + j], fz);
+        proof->tl.assign(hs, hs + w);
+        proof->tn.assign(hs + w, hs + 2 * w);
+        proof->qc.assign(hs + 2 * w, hs + 2 * w + q);
         T.end("compute opened values with Lagrange interpolation");
 
         T.begin("reduce rows");

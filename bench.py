@@ -342,7 +342,8 @@ def main_leg(args, dist, ranks_seen):
                                    "count": "w x [(h/2) log2 h (inverse) + N (coset twists) + (N/2) log2 h "
                                             "(8 forward coset NTTs of h)] Fr products",
                                    "peak_basis": "1024 SIMDs x 64 lanes / 4 cycles per v_mad_u64_u32 x 2.4 GHz / "
-                                                 "128 MADs per 8 x 32-bit Montgomery product"},
+                                                 "128 MADs per 8 x 32-bit Montgomery product",
+                                   "impl_mad_floor": ntt_impl_floor(frmul_gps, peak)},
                          "note": "VALU-bound: valu_issue = share of SIMD cycles issuing VALU in the NTT passes "
                                  "(PMC SQ_ACTIVE_INST_VALU, profiles/*_valu_pmc.json); HBM frac is low by design",
                          "algorithmic_bytes": lde_bytes, "ms": lde_ms},
@@ -608,6 +609,21 @@ def inflight(args, cfg, air, pub, trace, ctx, dtrace):
     return {"proofs_in_flight": P, "proofs": P * K, "value": P * K * h / dt, "unit": "trace-rows/s",
             "ms_per_proof": dt / (P * K) * 1e3,
             "note": "independent proofs on P streams of one GPU; value above is one proof at a time"}
+
+
+NTT_MADS_PER_PRODUCT = 162  # the NTT's 29-bit-limb product: 81 limb products + 81 reduction MADs
+
+
+def ntt_impl_floor(frmul_gps, peak):
+    """The LDE's products against the shipped multiplier's own MAD count (as
+    roofline_valu.impl_mad_floor does for Poseidon2): the kernel's distance from
+    an instruction stream of nothing but its products' MADs."""
+    if not peak:
+        return None
+    floor = peak["mad_per_s"] / NTT_MADS_PER_PRODUCT / 1e9
+    clk = peak["mperm_per_s_at_measured_clock"] / peak["mperm_per_s"]
+    return {"mads_per_product": NTT_MADS_PER_PRODUCT, "g_per_s": floor, "frac": frmul_gps / floor,
+            "frac_at_measured_clock": frmul_gps / (floor * clk)}
 
 
 def valu_peak():

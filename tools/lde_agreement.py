@@ -9,14 +9,16 @@ import csv, json, sys
 stats, bench = sys.argv[1], sys.argv[2]
 calls = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 rows = list(csv.DictReader(open(stats)))
-# the trace LDE (w = 8) runs the LOGCW = 3 instantiations; the quotient LDE (w = 4) the LOGCW = 2 ones
-logcw = int(sys.argv[4]) if len(sys.argv) > 4 else 3
+# which k_ntt_rm<DIF, MODE, LOGCW> instantiations belong to the LDE measured: "all" (the
+# probe runs only the trace LDE; since round 2 its passes use LOGCW 0 and 1), or one LOGCW
+# (round 1's bench trace: LOGCW 3 for the trace LDE, 2 for the quotient's)
+logcw = sys.argv[4] if len(sys.argv) > 4 else "all"
 lines, tot = [], 0.0
 for r in rows:
     name = r["Name"].replace("lsp::(anonymous namespace)::", "").replace("void ", "").split("(")[0]
     targs = name[name.find("<") + 1:-1].split(", ") if "<" in name else []
     # k_ntt_rm<DIF, MODE, LOGCW> (older traces: k_ntt_rm<DIF, MODE>)
-    ntt = "k_ntt_rm" in name and (len(targs) == 2 or targs[-1] == str(logcw))
+    ntt = "k_ntt_rm" in name and (logcw == "all" or len(targs) == 2 or targs[-1] == logcw)
     if ntt or "k_pow_tables" in name:
         ms = float(r["TotalDurationNs"]) / calls / 1e6
         tot += ms

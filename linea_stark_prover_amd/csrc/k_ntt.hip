@@ -55,6 +55,9 @@ struct NttPass {
     uint32_t xcd;       // 1: workgroup ids map to tiles XCD-aware (see k_ntt_rm)
     uint32_t twl_n;     // PASS_INV_FWD: forward twiddles cached in LDS (G (2^k - 1) entries; 0: read from tw)
     uint64_t narr;      // arrays (cosets) in dst
+    const Fr* ratio;    // PASS_INV_FWD, chained twist (nullptr: off): two-level table (L1, L2) of rho^row,
+                        // the ratio of consecutive coset shifts when the blocks run in order arr = bitrev(j)
+    uint32_t log_narr;  // with `ratio`: log2 narr
 };
 
 // element (row, col) of a pass's source through its column map; false: a
@@ -414,7 +417,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
     // twist factors; published by the barrier after the coefficient load below)
     uint4* twl = nullptr;
     if (FWD_FIRST && p.twl_n) {
-        const bool rt = !p.twist_per_col;
+        const bool rt = !p.twist_per_col || p.ratio;  // the row factors sit between the tile and these
         twl = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_raw) + (size_t)n_el * sizeof(F29) +
                                        (rt ? (size_t)(K << logG) * sizeof(F29) : 0));
         const uint32_t per = K - 1;  // entries per row group
@@ -456,12 +459,20 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
     }
     F29* fac = reinterpret_cast<F29*>(T.c + n_el);  // K * G extra entries (launcher sizes the LDS for it)
     const bool row_twist = FWD_FIRST && !p.twist_per_col;
-    for (uint32_t arr = arr0; arr < arr_end; ++arr) {
+    // Chained twist: coset blocks run in the order arr = bitrev(j), whose shifts
+    // are s rho^j, so block j's twisted coefficients are block j-1's times
+    // rho^row -- one product per element and block (the registers carry the
+    // running value) instead of the twist plus its factor from the two-level
+    // table.  rho^row is a row factor shared by every column, in `fac` from j = 1.
+    const bool chain = FWD_FIRST && p.ratio != nullptr;
+    for (uint32_t j = arr0; j < arr_end; ++j) {
+        const uint32_t arr = chain ? (uint32_t)brev_bits(j, p.log_narr) : j;
         Fr* base = p.dst + (size_t)arr * H * p.w;
-        if (FWD_FIRST) __syncthreads();  // the previous reads of the tile are done
-        // ---- twist factors s^row / h (29-bit form), once per row when every column shares the shift
-        if (row_twist) {
-            const Fr* tab = p.twist + (size_t)arr * ((1ull << p.L1) + (1ull << p.L2));
+        if (FWD_FIRST) __syncthreads();  // the previous reads of the tile (and of fac) are done
+        // ---- row factors (29-bit form): s^row / h once per row when every column
+        // shares the shift; with the chain, rho^row (computed once, at j = 1)
+        if (chain ? (j == 1 || (j == 0 && row_twist)) : row_twist) {
+            const Fr* tab = chain && j == 1 ? p.ratio : p.twist + (size_t)arr * ((1ull << p.L1) + (1ull << p.L2));
             for (uint32_t rg = threadIdx.x; rg < (K << logG); rg += NTT_THREADS) {
                 uint32_t t, g, c;
                 gm.split(rg << LOGCW, t, g, c);
@@ -472,19 +483,24 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
         // ---- load (twisting the registers, or from the array)
         if (FWD_FIRST) {
 #pragma unroll
-            for (uint32_t j = 0; j < NREG; ++j) {
-                const uint32_t e = threadIdx.x + j * NTT_THREADS;
+            for (uint32_t jr = 0; jr < NREG; ++jr) {
+                const uint32_t e = threadIdx.x + jr * NTT_THREADS;
                 uint32_t t, g, c;
                 gm.split(e, t, g, c);
                 if (e >= n_el || c >= cw) continue;
                 F29 f;
-                if (row_twist) {
+                if (row_twist || (chain && j > 0)) {
                     f = fac[(t << logG) + g];
                 } else {
                     const Fr* tab = p.twist + ((size_t)arr * p.w + c0 + c) * ((1ull << p.L1) + (1ull << p.L2));
                     f = pow2l29(tab, p.L1, gm.row_of(t, g));
                 }
-                T.put(gm.idx(t, g, c), f29_mul(xr[j], f));  // < 8.3 r
+                if (chain) {
+                    xr[jr] = f29_mul(xr[jr], f);  // < 8.2 r for inputs < 8.3 r and f < r, at every step
+                    T.put(gm.idx(t, g, c), xr[jr]);
+                } else {
+                    T.put(gm.idx(t, g, c), f29_mul(xr[jr], f));  // < 8.3 r
+                }
             }
         } else {
             for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
@@ -614,8 +630,11 @@ enum LdeWhat { LDE_FULL = 0, LDE_INV = 1, LDE_FWD = 2 };
 
 static hipError_t run_lde(LdeWhat what, const Fr* in, ColMap map, Fr* X, Fr* out, size_t w, uint32_t logh,
                           uint32_t ncosets, const uint4* tw_inv, const uint4* tw_fwd, const Fr* twist, uint32_t L1,
-                          uint32_t L2, int twist_per_col, hipStream_t st) {
+                          uint32_t L2, int twist_per_col, const Fr* ratio, hipStream_t st) {
     if (w == 0) return hipSuccess;
+    uint32_t log_narr = 0;
+    while ((1u << log_narr) < ncosets) ++log_narr;
+    if (ratio && (ncosets < 2 || (1u << log_narr) != ncosets)) return hipErrorInvalidValue;
     // Tile = 2^k positions x G groups x CW columns = 1024 elements (36 KiB of
     // LDS) where the array allows it, so every radix-4 group gives each of the
     // 256 threads one quad.  Up to k = 10 stages per pass with one column per
@@ -680,10 +699,12 @@ static hipError_t run_lde(LdeWhat what, const Fr* in, ColMap map, Fr* X, Fr* out
         p.nchunk = nchunk;
         p.canon = canon ? 1u : 0u;
         p.narr = narr;
+        p.ratio = mode == PASS_INV_FWD ? ratio : nullptr;
+        p.log_narr = log_narr;
         // the fused pass loops over the cosets inside each workgroup
         const uint64_t tiles = (uint64_t)(mode == PASS_INV_FWD ? 1 : narr) * ((1ull << logh) >> (k + logG)) * nchunk;
-        // tile, plus one twist factor per row in the fused pass
-        const bool fac = mode == PASS_INV_FWD && !twist_per_col;
+        // tile, plus one twist (or chain ratio) factor per row in the fused pass
+        const bool fac = mode == PASS_INV_FWD && (!twist_per_col || ratio);
         size_t lds = ((size_t(1) << (k + logG)) * CW + (fac ? (size_t(1) << (k + logG)) : 0)) * sizeof(F29);
         // ... and its forward twiddles when they fit (<= 512 entries, 24 KiB: 2 workgroups per CU)
         const size_t twl_n = (size_t(1) << logG) * ((size_t(1) << k) - 1);
@@ -753,20 +774,20 @@ static hipError_t run_lde(LdeWhat what, const Fr* in, ColMap map, Fr* X, Fr* out
 
 hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t ncosets, const uint4* tw_inv,
                       const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
-                      hipStream_t st) {
+                      const Fr* ratio, hipStream_t st) {
     return run_lde(LDE_FULL, in, ColMap::plain((uint32_t)w), X, out, w, logh, ncosets, tw_inv, tw_fwd, twist, L1, L2,
-                   twist_per_col, st);
+                   twist_per_col, ratio, st);
 }
 
 hipError_t launch_intt(const Fr* in, ColMap map, Fr* X, size_t w, uint32_t logh, const uint4* tw_inv, hipStream_t st) {
-    return run_lde(LDE_INV, in, map, X, nullptr, w, logh, 0, tw_inv, nullptr, nullptr, 0, 0, 0, st);
+    return run_lde(LDE_INV, in, map, X, nullptr, w, logh, 0, tw_inv, nullptr, nullptr, 0, 0, 0, nullptr, st);
 }
 
 hipError_t launch_lde_coeffs(const Fr* coef, ColMap map, Fr* out, size_t w, uint32_t logh, uint32_t ncosets,
                              const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
-                             hipStream_t st) {
+                             const Fr* ratio, hipStream_t st) {
     return run_lde(LDE_FWD, coef, map, nullptr, out, w, logh, ncosets, nullptr, tw_fwd, twist, L1, L2, twist_per_col,
-                   st);
+                   ratio, st);
 }
 
 hipError_t launch_fold_subcoset(const Fr* coef, ColMap map, size_t h, size_t S, uint32_t w, const Fr* fac, Fr* out,

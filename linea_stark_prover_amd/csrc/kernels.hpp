@@ -43,10 +43,13 @@ struct ColMap {
 // h * coefficients reduced below 2r).  tw_inv / tw_fwd: w_h^-x / w_h^x, x < h/2;
 // twist: two-level tables (L1, L2) of base s and scale 1/h, one per coset
 // (twist_per_col = 0) or per (coset, column) at index k*w + c -- all tables in
-// the 29-bit Montgomery form (launch_to_f29form; k_ntt.hip).
+// the 29-bit Montgomery form (launch_to_f29form; k_ntt.hip).  ratio (nullptr:
+// off; ncosets a power of two >= 2): the two-level table (L1, L2) of rho^i when
+// the shifts of blocks bitrev(0), bitrev(1), ... are s, s rho, s rho^2, ...; the
+// fused pass then uses only block 0's twist tables and chains the rest.
 hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uint32_t ncosets, const uint4* tw_inv,
                       const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
-                      hipStream_t st);
+                      const Fr* ratio, hipStream_t st);
 // The two halves of launch_lde, for a sharded proof whose ranks split the
 // inverse transform by columns (prove.cpp prove_shard):
 //   launch_intt       X (h x w) <- h * coefficients, natural order, of the w
@@ -56,7 +59,7 @@ hipError_t launch_lde(const Fr* in, Fr* X, Fr* out, size_t w, uint32_t logh, uin
 hipError_t launch_intt(const Fr* in, ColMap map, Fr* X, size_t w, uint32_t logh, const uint4* tw_inv, hipStream_t st);
 hipError_t launch_lde_coeffs(const Fr* coef, ColMap map, Fr* out, size_t w, uint32_t logh, uint32_t ncosets,
                              const uint4* tw_fwd, const Fr* twist, uint32_t L1, uint32_t L2, int twist_per_col,
-                             hipStream_t st);
+                             const Fr* ratio, hipStream_t st);
 // A sub-coset of the LDE (a sharded proof over more ranks than cosets):
 // out (S x w, row-major) = the h coefficients of every column folded to S,
 // out[i][c] = sum_t coef[i + t S][c] fac[c f + t] for t < f = h / S (coef read

@@ -183,6 +183,37 @@ static TwistTables lde_twist(lsp_ctx* ctx, size_t h, size_t w, uint32_t added_bi
     return T;
 }
 
+// The chained twist of the fused LDE pass (launch_lde's `ratio`): blocks
+// k0 + bitrev_a(j), j < nk = 2^a, k0 a multiple of nk, have the shifts
+// shift_c w_N^bitrev_b(k0) rho^j with rho = w_N^(2^b / nk), so the pass twists
+// block 0 from its table and every later block by rho^row.  The two-level table
+// of rho^i (29-bit form, cached in the context), or nullptr when the range is
+// not such a run or LSP_NTT_CHAIN=0 (A/B).
+static const Fr* chain_ratio(lsp_ctx* ctx, uint32_t logh, uint32_t added_bits, uint32_t k0, uint32_t nk) {
+    static const bool on = [] {
+        const char* e = std::getenv("LSP_NTT_CHAIN");
+        return !(e && *e == '0');
+    }();
+    if (!on || logh == 0 || nk < 2 || (nk & (nk - 1)) != 0 || k0 % nk != 0 || nk > (1u << added_bits)) return nullptr;
+    const uint32_t logN = logh + added_bits;
+    const Fr rho = fr_pow_u64(host_two_adic_generator(logN), (1ull << added_bits) / nk);
+    uint32_t L1, L2;
+    two_level(logh, L1, L2);
+    char key[112];
+    std::snprintf(key, sizeof key, "ldechain_%u_%08x%08x%08x%08x%08x%08x%08x%08x", logh, rho.v[7], rho.v[6], rho.v[5],
+                  rho.v[4], rho.v[3], rho.v[2], rho.v[1], rho.v[0]);
+    auto it = ctx->ptabs.find(key);
+    if (it != ctx->ptabs.end()) return it->second;
+    Fr* tab = ctx->fbuf(key, (1ull << L1) + (1ull << L2));
+    Fr* b = ctx->fbuf("ldechain_base", 1);
+    LSP_HIP(hipMemcpyAsync(b, &rho, sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+    LSP_HIP(launch_pow_tables(b, 1, L1, L2, nullptr, tab, ctx->stream));
+    LSP_HIP(launch_to_f29form(tab, tab, (1ull << L1) + (1ull << L2), ctx->stream));
+    LSP_HIP(hipStreamSynchronize(ctx->stream));  // `rho` is a host temporary
+    ctx->ptabs[key] = tab;
+    return tab;
+}
+
 // Coset blocks [k0, k0 + nk) of the bit-reversed LDE (nk = 0: all
 // 2^added_bits): block k = rows k*h .. (k+1)*h - 1 of the full LDE, the
 // evaluations on shift_c * w_N^bitrev(k) * H_h.  d_out receives nk blocks.
@@ -196,7 +227,7 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
     Fr* X = ctx->fbuf("lde_X", h * w);
     const TwistTables T = lde_twist(ctx, h, w, added_bits, shifts_host, k0, nk);
     LSP_HIP(launch_lde(d_in, X, d_out, w, logh, nk, ctx->twiddle29(logh, true), ctx->twiddle29(logh, false), T.tabs,
-                       T.L1, T.L2, T.shared ? 0 : 1, ctx->stream));
+                       T.L1, T.L2, T.shared ? 0 : 1, chain_ratio(ctx, logh, added_bits, k0, nk), ctx->stream));
 }
 
 // The same blocks from h * coefficients (natural order) at `coef`, laid out
@@ -207,7 +238,7 @@ static void lde_coeffs_device(lsp_ctx* ctx, const Fr* coef, ColMap map, size_t h
     LSP_REQUIRE(k0 + nk <= (1u << added_bits) && logh >= 1, LSP_E_ARG, "coset range outside the LDE");
     const TwistTables T = lde_twist(ctx, h, w, added_bits, shifts_host, k0, nk, div_h);
     LSP_HIP(launch_lde_coeffs(coef, map, d_out, w, logh, nk, ctx->twiddle29(logh, false), T.tabs, T.L1, T.L2,
-                              T.shared ? 0 : 1, ctx->stream));
+                              T.shared ? 0 : 1, chain_ratio(ctx, logh, added_bits, k0, nk), ctx->stream));
 }
 
 // TwoAdicSubgroupDft::coset_dft_batch ([EXT p3-dft]; dft_batch: shift 1): the

@@ -166,6 +166,14 @@ template <int K> __global__ __launch_bounds__(256) void kr(Sample* out, unsigned
 #define HL(x, y) asm volatile("v_mul_hi_u32 %0, %0, %2\n\tv_mul_lo_u32 %1, %1, %2" : "+v"(x), "+v"(y) : "v"(b))
             HL(u0, u1); HL(u2, u3); HL(u4, u5); HL(u6, u7);
 #undef HL
+        } else if (K == 34) {  // v_mad_i64_i32 (signed; the signed-digit product)
+#define MSI(c) asm volatile("v_mad_i64_i32 %0, s[40:41], %1, %2, %0" : "+v"(c) : "v"(a), "v"(b) : "s40", "s41")
+            MSI(c0); MSI(c1); MSI(c2); MSI(c3); MSI(c4); MSI(c5); MSI(c6); MSI(c7);
+#undef MSI
+        } else if (K == 35) {  // v_ashrrev_i64 (the signed carries)
+#define AS(c) asm volatile("v_ashrrev_i64 %0, 29, %0" : "+v"(c))
+            AS(c0); AS(c1); AS(c2); AS(c3); AS(c4); AS(c5); AS(c6); AS(c7);
+#undef AS
         } else if (K == 17) {  // v_sub_u32 chains on a 64-bit pair: v_sub_co_u32 / v_subb_co_u32 (8 instructions)
 #define SB(x, y) asm volatile("v_sub_co_u32 %0, vcc, %0, %2\n\tv_subb_co_u32 %1, vcc, %1, %2, vcc" : "+v"(x), "+v"(y) : "v"(a) : "vcc")
             SB(u0, u1); SB(u2, u3); SB(u4, u5); SB(u6, u7);
@@ -254,6 +262,8 @@ int main(int argc, char** argv) {
     rows.push_back(run<31>("v_mad_u64_u32 + v_lshrrev_b64 (1:1)", out, sink, cus));
     rows.push_back(run<32>("v_fma_f64 + v_add_u32 (1:1)", out, sink, cus));
     rows.push_back(run<33>("v_mul_hi_u32 + v_mul_lo_u32 (1:1)", out, sink, cus));
+    rows.push_back(run<34>("v_mad_i64_i32", out, sink, cus));
+    rows.push_back(run<35>("v_ashrrev_i64", out, sink, cus));
     printf("device %s, %d CUs; cycles per wave64 instruction per SIMD (shader clock, s_memtime), "
            "median over waves; GHz = s_memtime / s_memrealtime\n", pr.gcnArchName, cus);
     printf("%-34s %21s   %27s   %s\n", "", "per-wave median", "whole-grid span", "");

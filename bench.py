@@ -109,6 +109,10 @@ def parse(argv=None):
     ap.add_argument("--shape-leg", default="6",
                     help="ncols of the extra 2^log_n leg in bench.log's shape (6+6 columns, w = 14, the "
                          "reference's only measured run, bench.log:18-20); 'none' to skip")
+    ap.add_argument("--shape-pow-bits", type=int, default=0,
+                    help="the shape leg once more with this many proof-of-work bits (29: bench.log's run, which "
+                         "ground a witness, bench.log:65, 19.3 s; bin/src/main.rs:62 sets 0 with the comment "
+                         "//29); 0 skips")
     ap.add_argument("--shard", action="store_true", help="main leg: one proof sharded over the N ranks (C4)")
     ap.add_argument("--comm", choices=["rccl", "gloo"], default="rccl", help="--shard exchange transport")
     ap.add_argument("--shard-leg", default="auto",
@@ -465,14 +469,56 @@ def shape_leg(args, dist, ctx, ncols):
     finally:
         ctx.dev_free(dtrace)
     t = elapsed / args.steps
-    return {"workload": f"{ncols}x{ncols} permutation AIR, 2^{args.log_n} rows (w={w}, q="
-                        f"{1 << air_log_q(air, cfg)}): the shape of bench.log:18-20",
-            "steps": args.steps, "warmup": max(args.warmup, 1), "prove_time_s": t,
-            "prove_time_median_s": statistics.median(step_s) if step_s else None,
-            "value": h / t, "unit": "trace-rows/s", "verified": bool(ctx.verify(proof, air, pub)),
-            "phases_ms": phases,
-            "reference_s": 342.0, "reference_source": "bench.log:18 (6+6 columns, w = 14, 2^19 rows, CPU)",
-            "speedup_vs_reference": 342.0 / t if args.log_n == 19 else None}
+    out = {"workload": f"{ncols}x{ncols} permutation AIR, 2^{args.log_n} rows (w={w}, q="
+                       f"{1 << air_log_q(air, cfg)}): the shape of bench.log:18-20",
+           "steps": args.steps, "warmup": max(args.warmup, 1), "prove_time_s": t,
+           "prove_time_median_s": statistics.median(step_s) if step_s else None,
+           "value": h / t, "unit": "trace-rows/s", "verified": bool(ctx.verify(proof, air, pub)),
+           "phases_ms": phases, "proof_of_work_bits": cfg.proof_of_work_bits,
+           "reference_s": 342.0, "reference_source": "bench.log:18 (6+6 columns, w = 14, 2^19 rows, CPU)",
+           "speedup_vs_reference": 342.0 / t if args.log_n == 19 else None}
+    if args.shape_pow_bits > 0:
+        try:
+            out["with_pow"] = shape_pow_leg(args, dist, ctx, ncols, args.shape_pow_bits)
+        except Exception as e:  # the leg above is still reported
+            out["with_pow"] = {"error": f"{type(e).__name__}: {e}"}
+    return out
+
+
+def shape_pow_leg(args, dist, ctx, ncols, bits):
+    """bench.log's run ground a proof-of-work witness (bench.log:65: 19.3 s of its
+    342 s), which bin/src/main.rs:62 now sets to 0 bits with the comment //29: the
+    same shape with `bits` bits on a context of its own (the grind is part of
+    every timed proof; the witness is fixed by the transcript, so every step does
+    the same work).  1 warm-up + 2 timed proofs."""
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import Context, StarkConfig
+    from linea_stark_prover_amd.replicas import timed_steps
+    import numpy as np
+    cfg = StarkConfig(seed=args.seed, proof_of_work_bits=bits)
+    a, d, _ = cfg.seeded()
+    pub = np.concatenate([a, d])
+    air = permutation_air(ncols)
+    w, h = 2 * ncols + 2, 1 << args.log_n
+    c = Context(cfg, device=ctx.device)
+    try:
+        dtrace = c.gen_permutation_trace_device(args.log_n, ncols, a, d, seed=args.seed)
+        try:
+            step = lambda: c.prove(dtrace, air, pub, h, w)  # noqa: E731
+            elapsed, proof = timed_steps(step, 2, 1, dist, sync=c.synchronize)
+            phases = dict(c.last_timings())
+        finally:
+            c.dev_free(dtrace)
+        t = elapsed / 2
+        return {"proof_of_work_bits": bits, "steps": 2, "warmup": 1, "prove_time_s": t,
+                "grind_ms": round(phases.get("grind for proof-of-work witness", float("nan")), 3),
+                "verified": bool(c.verify(proof, air, pub)),
+                "reference_s": 342.0, "reference_grind_s": 19.3,
+                "speedup_vs_reference": 342.0 / t if args.log_n == 19 else None,
+                "note": "the grind is one Poseidon2 permutation per candidate witness (k_grind), "
+                        "smallest witness first, as HashChallenger::grind"}
+    finally:
+        c.close()
 
 
 def shard_leg_sizes(args, world):

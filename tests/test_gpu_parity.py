@@ -394,7 +394,7 @@ def test_prove_large_self_consistency(gpu_ctx):
     assert gpu_ctx.verify(pf1, air, pub)
 
 
-@pytest.mark.parametrize("bits", [1, 8, 13])
+@pytest.mark.parametrize("bits", [1, 8, 13, 20])
 def test_prove_with_pow_grinding_matches_oracle(oracle_lib, bits):
     """F2: GPU grinding finds the same (smallest) witness as the oracle."""
     from linea_stark_prover_amd.air import permutation_air

@@ -104,12 +104,16 @@ def parse(argv=None):
                          "wide AIR (4 LogUp lookups + 8 permutation groups of 6+6, W = 184)")
     ap.add_argument("--seed", type=int, default=0x4C494E4541)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-log-n", type=int, default=16, help="CPU-baseline sample size (rows = 2^cpu_log_n)")
-    ap.add_argument("--cpu-runs", type=int, default=5, help="CPU-baseline timed runs (median; after 1 warm-up)")
+    ap.add_argument("--cpu-log-n", type=int, default=None,
+                    help="CPU-baseline size (rows = 2^cpu_log_n; default: the headline's --log-n, BASELINE.md's "
+                         "2^19 input)")
+    ap.add_argument("--cpu-runs", type=int, default=3, help="CPU-baseline timed runs (median; after 1 warm-up)")
+    ap.add_argument("--cpu-small-log-n", type=int, default=16,
+                    help="an extra, smaller CPU sample reported beside the headline one (0 disables)")
     ap.add_argument("--shape-leg", default="6",
                     help="ncols of the extra 2^log_n leg in bench.log's shape (6+6 columns, w = 14, the "
                          "reference's only measured run, bench.log:18-20); 'none' to skip")
-    ap.add_argument("--shape-pow-bits", type=int, default=0,
+    ap.add_argument("--shape-pow-bits", type=int, default=29,
                     help="the shape leg once more with this many proof-of-work bits (29: bench.log's run, which "
                          "ground a witness, bench.log:65, 19.3 s; bin/src/main.rs:62 sets 0 with the comment "
                          "//29); 0 skips")
@@ -131,6 +135,8 @@ def parse(argv=None):
     ap.add_argument("--batch-leg-steps", type=int, default=2)
     ap.add_argument("--device", type=int, default=None, help="GPU of this rank (default: LOCAL_RANK mod #GPUs)")
     ap.add_argument("--dump-proof", default=None, help="rank 0 writes the last proof here")
+    ap.add_argument("--dump-batch-proofs", default=None,
+                    help="every rank writes its batch-leg proof to <this>.<rank>.<log_n>.bin")
     ap.add_argument("--dump-comm-schedule", default=None,
                     help="--shard --comm gloo: every rank writes the collectives its communicator carried, in "
                          "order, to <this>.<rank>.json")
@@ -205,7 +211,10 @@ def main():
             out["sharded"] = sharded
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline and args.air == "perm":
-            out["cpu_baseline"] = cpu_baseline(args)
+            cb = cpu_baseline(args)
+            if cb["log_n"] == args.log_n:
+                cb["gpu_speedup"] = out["value"] / cb["value"]
+            out["cpu_baseline"] = cb
         print(json.dumps(out), flush=True)
     ctx.close()
     dist.close()
@@ -430,14 +439,19 @@ def batch_leg(args, dist, ctx, sizes):
         step = lambda: ctx.prove(dtrace, air, pub, h, w)  # noqa: E731
         elapsed, proof = timed_steps(step, args.batch_leg_steps, 1, dist, sync=ctx.synchronize)
         ctx.dev_free(dtrace)
+        if args.dump_batch_proofs:
+            with open(f"{args.dump_batch_proofs}.{dist.rank}.{log_n}.bin", "wb") as f:
+                f.write(proof)
+        ok = bool(ctx.verify(proof, air, pub))  # every rank checks its own proof
+        nok = int(round(dist.sum(1.0 if ok else 0.0)))
         run = {"log_n": log_n, "rows_per_rank": h, "steps": args.batch_leg_steps, "warmup": 1,
                "prove_time_s": elapsed / args.batch_leg_steps,
                "value": dist.world * h * args.batch_leg_steps / elapsed, "unit": "trace-rows/s",
                "scaling": "weak",
                "workload": f"{args.ncols}x{args.ncols} permutation AIR, one independent 2^{log_n}-row proof per "
                            f"rank ({dist.world} rank(s))"}
-        if dist.rank == 0:
-            run["verified"] = bool(ctx.verify(proof, air, pub))
+        run["verified"] = nok == dist.world
+        run["verified_ranks"] = nok
         runs.append(run)
     return {"runs": runs}
 
@@ -510,8 +524,20 @@ def shape_pow_leg(args, dist, ctx, ncols, bits):
         finally:
             c.dev_free(dtrace)
         t = elapsed / 2
+        grind_ms = phases.get("grind for proof-of-work witness", float("nan"))
+        witness = pow_witness(proof)
+        # the device grinds 2^22 candidates per launch (prove.cpp grind_device),
+        # smallest first: the candidates this proof tested, their rate, and the
+        # expected cost at `bits` (2^bits candidates) -- one proof's grind_ms is
+        # one draw of a geometric witness, not the cost
+        batch = 1 << 22
+        tested = (witness // batch + 1) * batch
+        rate = tested / (grind_ms * 1e-3) if grind_ms == grind_ms and grind_ms > 0 else None
         return {"proof_of_work_bits": bits, "steps": 2, "warmup": 1, "prove_time_s": t,
-                "grind_ms": round(phases.get("grind for proof-of-work witness", float("nan")), 3),
+                "grind_ms": round(grind_ms, 3), "witness": witness, "candidates_tested": tested,
+                "candidates_per_s": rate,
+                "expected_grind_ms": (2 ** bits) / rate * 1e3 if rate else None,
+                "expected_prove_time_s": t - grind_ms * 1e-3 + (2 ** bits) / rate if rate else None,
                 "verified": bool(c.verify(proof, air, pub)),
                 "reference_s": 342.0, "reference_grind_s": 19.3,
                 "speedup_vs_reference": 342.0 / t if args.log_n == 19 else None,
@@ -519,6 +545,16 @@ def shape_pow_leg(args, dist, ctx, ncols, bits):
                         "smallest witness first, as HashChallenger::grind"}
     finally:
         c.close()
+
+
+def pow_witness(proof: bytes) -> int:
+    """the proof-of-work witness of a serialized proof (csrc/proof.cpp layout:
+    header, 2 roots, 2w + q opened values, FRI roots, final polynomial, then
+    the witness, canonical little-endian)"""
+    import struct
+    _log_h, log_q, w, _nq, nr, nf = struct.unpack_from("<6I", proof, 8)
+    off = 8 + 24 + 32 * (2 + 2 * w + (1 << log_q) + nr + nf)
+    return int.from_bytes(proof[off:off + 32], "little")
 
 
 def shard_leg_sizes(args, world):
@@ -601,11 +637,14 @@ def shard_leg(args, dist, ctx, sizes):
         elapsed, proof = timed_steps(step, args.shard_leg_steps, args.shard_leg_warmup, dist,
                                      sync=ctx.synchronize)
         ctx.dev_free(dtrace)
+        table = collective_table(ctx, dist) if world > 1 else None
         run = {"log_n": log_n, "rows": h, "steps": args.shard_leg_steps, "warmup": args.shard_leg_warmup,
                "prove_time_s": elapsed / args.shard_leg_steps,
                "value": h * args.shard_leg_steps / elapsed, "unit": "trace-rows/s",
                "workload": f"{args.ncols}x{args.ncols} permutation AIR, 2^{log_n} rows, one proof over {world} "
                            f"rank(s)", "proof_bytes": len(proof) if proof else 0}
+        if table is not None:
+            run.update(table)
         if rank == 0:
             t = time.perf_counter()
             run["verified"] = bool(ctx.verify(proof, air, pub))
@@ -615,6 +654,32 @@ def shard_leg(args, dist, ctx, sizes):
         from linea_stark_prover_amd import shard as S
         S.detach(ctx)
     return res
+
+
+def collective_table(ctx, dist):
+    """The last sharded proof's collectives on every rank (lsp_comm_log): one
+    row per collective in issue order -- op, bytes per rank, root, what it
+    carried, and each rank's device ms around it (the wait for the slowest
+    peer included) -- plus each rank's communicator creation time, so an
+    8-GPU run's curve can be read exchange by exchange.  `schedule_identical`
+    checks what RCCL needs: every rank issued the same (op, bytes, root)
+    sequence."""
+    log, init_ms = ctx.comm_log()
+    logs = dist.all_gather_object((log, init_ms))
+    ref = [(e["op"], e["bytes"], e["root"]) for e in logs[0][0]]
+    same = all([(e["op"], e["bytes"], e["root"]) for e in lg] == ref for lg, _ in logs)
+    rows = []
+    for i, e in enumerate(logs[0][0]):
+        rows.append({"op": e["op"], "bytes": e["bytes"], "root": e["root"], "tag": e["tag"],
+                     "ms_by_rank": [round(lg[i]["ms"], 3) if i < len(lg) else None for lg, _ in logs]})
+    by_tag = {}
+    for r in rows:
+        t = by_tag.setdefault(r["tag"], {"count": 0, "bytes": 0, "max_rank_ms": 0.0})
+        t["count"] += 1
+        t["bytes"] += r["bytes"]
+        t["max_rank_ms"] = round(t["max_rank_ms"] + max(x for x in r["ms_by_rank"] if x is not None), 3)
+    return {"collectives": rows, "collectives_by_tag": by_tag, "schedule_identical": same,
+            "comm_init_ms_by_rank": [round(i, 3) for _, i in logs]}
 
 
 def inflight(args, cfg, air, pub, trace, ctx, dtrace):
@@ -788,35 +853,56 @@ def cpu_share() -> int:
     return min(n, omp) if omp > 0 else n
 
 
+def _cpu_prove_times(cref, args, log_n, runs, threads):
+    """warm-up + `runs` timed full proofs of the C restatement at 2^log_n rows"""
+    p = cref.setup(args.seed)
+    tb, w = cref.gen_perm_trace(p, log_n, args.ncols, seed=args.seed)
+    air = cref.perm_air(args.ncols)
+    ts = []
+    for k in range(runs + 1):
+        t = time.perf_counter()
+        cref.prove(p, tb, 1 << log_n, w, air, nthreads=threads)
+        dt = time.perf_counter() - t
+        if k:  # run 0 is the warm-up
+            ts.append(dt)
+        # progress on stderr: a 2^19 CPU proof takes tens of seconds
+        print(f"[cpu_baseline] 2^{log_n} {'warm-up' if not k else f'run {k}/{runs}'}: {dt:.2f} s",
+              file=sys.stderr, flush=True)
+    return ts
+
+
 def cpu_baseline(args):
-    """The oracle's C restatement proving the headline workload's AIR
-    (2^cpu_log_n rows) on the host (test infrastructure used only as the
-    reported baseline), one thread per core of this process's CPU share: one
-    warm-up, then the median of --cpu-runs timed proofs."""
+    """The oracle's C restatement (test infrastructure, used here only as the
+    reported baseline) proving the headline workload -- the same AIR, size,
+    conventions and seed (the 2^19 input) -- on the host, one
+    thread per core of this process's CPU share: one warm-up, then the median
+    of --cpu-runs timed proofs.  A smaller sample (--cpu-small-log-n) is
+    reported beside it under `small_sample`."""
     from oracle import cref
     cref.build()
     threads = cpu_share()
-    p = cref.setup(args.seed)
-    tb, w = cref.gen_perm_trace(p, args.cpu_log_n, args.ncols, seed=args.seed)
-    air = cref.perm_air(args.ncols)
-    cref.prove(p, tb, 1 << args.cpu_log_n, w, air, nthreads=threads)  # warm-up
-    ts = []
-    for _ in range(max(args.cpu_runs, 1)):
-        t = time.perf_counter()
-        cref.prove(p, tb, 1 << args.cpu_log_n, w, air, nthreads=threads)
-        ts.append(time.perf_counter() - t)
+    log_n = args.cpu_log_n if args.cpu_log_n is not None else args.log_n
+    runs = max(args.cpu_runs, 1)
+    ts = _cpu_prove_times(cref, args, log_n, runs, threads)
     dt = statistics.median(ts)
     try:
         nproc = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
     except (OSError, ValueError):
         nproc = None
-    return {"value": (1 << args.cpu_log_n) / dt, "unit": "trace-rows/s", "cores": threads, "kind": "port",
-            "seconds": dt, "seconds_runs": [round(x, 3) for x in ts], "warmup": 1, "nproc": nproc,
-            "machine_cpus": os.cpu_count(), "cpu_model": cpu_model(),
-            "sample": f"oracle/lsp_oracle.c full prove, {args.ncols}x{args.ncols} permutation AIR at "
-                      f"2^{args.cpu_log_n} rows (same AIR, conventions and seed as the headline; a bounded "
-                      f"sample of its 2^{args.log_n}-row workload), median of {len(ts)} runs after 1 warm-up, "
-                      f"{threads} threads = this process's CPU share (affinity / OMP_NUM_THREADS)"}
+    out = {"value": (1 << log_n) / dt, "unit": "trace-rows/s", "cores": threads, "kind": "port",
+           "seconds": dt, "seconds_runs": [round(x, 3) for x in ts], "warmup": 1, "log_n": log_n, "nproc": nproc,
+           "machine_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+           "sample": f"oracle/lsp_oracle.c full prove of the headline workload: {args.ncols}x{args.ncols} "
+                     f"permutation AIR at 2^{log_n} rows (same AIR, conventions and seed as the GPU line), "
+                     f"median of {len(ts)} runs after 1 warm-up, {threads} threads = this process's CPU share "
+                     f"(affinity / OMP_NUM_THREADS)",
+           "gpu_speedup": None}
+    if args.cpu_small_log_n and args.cpu_small_log_n < log_n:
+        ts2 = _cpu_prove_times(cref, args, args.cpu_small_log_n, 3, threads)
+        out["small_sample"] = {"log_n": args.cpu_small_log_n, "seconds": statistics.median(ts2),
+                               "value": (1 << args.cpu_small_log_n) / statistics.median(ts2),
+                               "seconds_runs": [round(x, 3) for x in ts2]}
+    return out
 
 
 if __name__ == "__main__":

@@ -65,7 +65,8 @@ int main(int argc, char** argv) {
     CHECK(lsp_log_quotient_degree(air, k, 1, &log_q), NULL);
 
     lsp_params p;
-    memset(&p, 0, sizeof p);
+    memset(&p, 0, sizeof p); /* zero = the default transcript conventions (U7/U8/U12) */
+    p.struct_size = (uint32_t)sizeof p;
     p.sbox_degree = 11;
     p.rounds_f = rounds_f;
     p.rounds_p = rounds_p;

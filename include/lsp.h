@@ -66,8 +66,14 @@ typedef struct lsp_tree lsp_tree;
 typedef struct lsp_proof lsp_proof;
 
 /* StarkConfig / FriConfig / Perm parameters (bin/src/config.rs:9-25,
- * bin/src/main.rs:49-64). */
+ * bin/src/main.rs:49-64).
+ * struct_size must be sizeof(lsp_params) as the caller compiled it (88
+ * bytes on LP64 for this layout): lsp_ctx_create rejects any other
+ * value with LSP_E_ARG, so a caller built against an older layout (whose
+ * first field was sbox_degree = 11 or 17) fails loudly instead of having
+ * its stack read as the newer fields. */
 typedef struct {
+    uint32_t struct_size;          /* sizeof(lsp_params) */
     uint32_t sbox_degree;          /* U1: 11 (default) or 17 */
     uint32_t rounds_f;             /* full rounds, 8 (bin/src/main.rs:49) */
     uint32_t rounds_p;             /* partial rounds, 22 (bin/src/main.rs:49) */
@@ -92,6 +98,27 @@ typedef struct {
      * (additions only) on every path: device, host scalar and host IFMA. */
     const lsp_fr *internal_diag;
     const lsp_fr *external_mds;
+    /* Transcript conventions of the fork's p3-uni-stark / p3-fri /
+     * HashChallenger ([EXT], bin/src/config.rs:23, bin/src/main.rs:78,88-96),
+     * which no reference artefact pins.  0 = the
+     * default for every field, so a zero-filled tail keeps today's proofs.
+     *   U7  skip_log_degree        1: log2(h) is not observed before the trace root
+     *       skip_public_values     1: the public values [alpha, delta] are not
+     *                              observed before the quotient challenge
+     *       observe_opened_values  1: TwoAdicFriPcs::open observes every opened
+     *                              value (trace at zeta, trace at zeta*w_h,
+     *                              chunk j at zeta, in that order) before it
+     *                              samples alpha_fri (later upstream Plonky3)
+     *   U8  sample_bits_montgomery 1: sample_bits (query indices and the PoW
+     *                              check) takes the low bits of the Montgomery
+     *                              form instead of the canonical value
+     *   U12 skip_final_poly        1: the final polynomial's coefficients are
+     *                              not observed before grinding */
+    uint32_t skip_log_degree;
+    uint32_t skip_public_values;
+    uint32_t observe_opened_values;
+    uint32_t sample_bits_montgomery;
+    uint32_t skip_final_poly;
 } lsp_params;
 
 /* ---------------------------------------------------------------- library */
@@ -277,8 +304,11 @@ int lsp_ctx_detach_comm(lsp_ctx *ctx);
 /* Rehearsal transport: this context plays rank `rank` of a `size`-rank
  * lsp_prove_sharded on its one GPU, every peer's part of an exchange
  * fabricated locally (allgather slots of other ranks = a copy of this rank's
- * payload, broadcasts from other roots = zeros).  The proof is NOT valid; the
- * call measures one rank's device memory and phase times at full size (e.g.
+ * payload, broadcasts from other roots = zeros).  The proof is NOT valid and
+ * is marked so: lsp_proof_serialize answers only the size query (buf = NULL)
+ * and lsp_proof_get_view refuses it (LSP_E_STATE).  The call measures one
+ * rank's device memory, phase times and collective schedule (lsp_comm_log) at
+ * full size (e.g.
  * BASELINE configs[3], 2^26 rows over 8 GPUs, one rank at a time on one GPU;
  * tools/rank_rehearsal.py). */
 int lsp_ctx_attach_loopback(lsp_ctx *ctx, int rank, int size);
@@ -291,6 +321,20 @@ int lsp_ctx_mem_stats(lsp_ctx *ctx, size_t *pool_bytes, size_t *device_used, siz
 int lsp_comm_selftest(lsp_ctx *ctx);
 /* rank and size of the attached communicator (LSP_E_STATE if none) */
 int lsp_comm_info(lsp_ctx *ctx, int *rank, int *size);
+/* The collective schedule of the last lsp_prove_sharded on ctx, one entry
+ * per collective in issue order: ops[i] 'A' (allgather; bytes[i] = each
+ * rank's share) or 'B' (broadcast; bytes[i] = the buffer, roots[i] = its
+ * root; -1 for allgathers), tags[i] what it carried ("trace coefficients",
+ * "quotient chunk coefficients", "trace subtree roots", "FRI vector", ...;
+ * strings live until the next prove on ctx), ms[i] the device time between
+ * events recorded around it on ctx's stream (the wait for the slowest peer
+ * included).  init_ms = the communicator's creation time (RCCL:
+ * ncclCommInitRank; 0 for the other transports).  Any output array may be
+ * NULL; *n = the number of entries (at most cap are written).  Every rank of
+ * a proof must log the same (op, bytes, root) sequence: RCCL hangs otherwise
+ * (tests/test_gpu_configs_full.py checks it at BASELINE configs[3]'s size). */
+int lsp_comm_log(lsp_ctx *ctx, char *ops, size_t *bytes, int *roots, double *ms, const char **tags, size_t cap,
+                 size_t *n, double *init_ms);
 int lsp_prove_sharded(lsp_ctx *ctx, const lsp_fr *trace, size_t h, size_t w, const int32_t *air, size_t air_len,
                       const lsp_fr *public_values, size_t npub, int mem, lsp_proof **out);
 /* serialized proof (format in DESIGN.md); buf == NULL -> *len = required size */

@@ -20,11 +20,24 @@ c_fr_p = ctypes.c_void_p  # lsp_fr* (32-byte elements)
 
 
 class LspParams(ctypes.Structure):
-    _fields_ = [("sbox_degree", ctypes.c_uint32), ("rounds_f", ctypes.c_uint32), ("rounds_p", ctypes.c_uint32),
+    """include/lsp.h lsp_params; keyword construction, struct_size filled in.
+    The U7/U8/U12 transcript switches default to 0 (SURVEY 8(c)'s choices)."""
+    _fields_ = [("struct_size", ctypes.c_uint32),
+                ("sbox_degree", ctypes.c_uint32), ("rounds_f", ctypes.c_uint32), ("rounds_p", ctypes.c_uint32),
                 ("round_constants", ctypes.c_void_p), ("log_blowup", ctypes.c_uint32),
                 ("log_final_poly_len", ctypes.c_uint32), ("num_queries", ctypes.c_uint32),
                 ("proof_of_work_bits", ctypes.c_uint32), ("public_degree", ctypes.c_int32),
-                ("internal_diag", ctypes.c_void_p), ("external_mds", ctypes.c_void_p)]
+                ("internal_diag", ctypes.c_void_p), ("external_mds", ctypes.c_void_p),
+                ("skip_log_degree", ctypes.c_uint32), ("skip_public_values", ctypes.c_uint32),
+                ("observe_opened_values", ctypes.c_uint32), ("sample_bits_montgomery", ctypes.c_uint32),
+                ("skip_final_poly", ctypes.c_uint32)]
+
+    def __init__(self, **kw):
+        super().__init__(struct_size=ctypes.sizeof(LspParams), **kw)
+
+
+TRANSCRIPT_SWITCHES = ("skip_log_degree", "skip_public_values", "observe_opened_values", "sample_bits_montgomery",
+                       "skip_final_poly")
 
 
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
@@ -116,6 +129,10 @@ _SIGS = {
                                                 ctypes.c_size_t]),
     "lsp_comm_selftest": (ctypes.c_int, [ctypes.c_void_p]),
     "lsp_comm_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "lsp_comm_log": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_size_t),
+                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double),
+                                    ctypes.POINTER(ctypes.c_char_p), ctypes.c_size_t,
+                                    ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_double)]),
     "lsp_prove_sharded": (ctypes.c_int, [ctypes.c_void_p, c_fr_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p,
                                          ctypes.c_size_t, c_fr_p, ctypes.c_size_t, ctypes.c_int,
                                          ctypes.POINTER(ctypes.c_void_p)]),

@@ -150,6 +150,12 @@ void lsp_two_adic_generator(uint32_t bits, lsp_fr* out) {
 int lsp_ctx_create(int device, const lsp_params* p, lsp_ctx** out) {
     return guarded(nullptr, [&] {
         LSP_REQUIRE(p && out && p->round_constants, LSP_E_ARG, "null params");
+        LSP_REQUIRE(p->struct_size == sizeof(lsp_params), LSP_E_ARG,
+                    "lsp_params.struct_size must be sizeof(lsp_params) of this header (caller built against "
+                    "another lsp.h?)");
+        LSP_REQUIRE(p->skip_log_degree <= 1 && p->skip_public_values <= 1 && p->observe_opened_values <= 1 &&
+                        p->sample_bits_montgomery <= 1 && p->skip_final_poly <= 1,
+                    LSP_E_ARG, "transcript switches are 0 or 1");
         LSP_REQUIRE(p->sbox_degree == 11 || p->sbox_degree == 17, LSP_E_ARG, "S-box degree must be 11 or 17");
         LSP_REQUIRE(p->rounds_f >= 2 && p->rounds_f % 2 == 0 && p->rounds_f <= 64 && p->rounds_p <= 256, LSP_E_ARG,
                     "bad round counts");
@@ -209,6 +215,11 @@ int lsp_ctx_create(int device, const lsp_params* p, lsp_ctx** out) {
         c->num_queries = p->num_queries;
         c->pow_bits = p->proof_of_work_bits;
         c->public_degree = p->public_degree;
+        c->transcript.log_degree = !p->skip_log_degree;
+        c->transcript.public_values = !p->skip_public_values;
+        c->transcript.opened_values = p->observe_opened_values != 0;
+        c->transcript.mont_bits = p->sample_bits_montgomery != 0;
+        c->transcript.final_poly = !p->skip_final_poly;
         *out = c.release();
     });
 }
@@ -914,6 +925,28 @@ int lsp_comm_info(lsp_ctx* ctx, int* rank, int* size) {
     });
 }
 
+int lsp_comm_log(lsp_ctx* ctx, char* ops, size_t* bytes, int* roots, double* ms, const char** tags, size_t cap,
+                 size_t* n, double* init_ms) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && n, LSP_E_ARG, "null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        LSP_REQUIRE(ctx->comm, LSP_E_STATE, "no communicator attached");
+        need_gpu(ctx);
+        Comm& c = *ctx->comm;
+        c.resolve_log();
+        *n = c.log.size();
+        if (init_ms) *init_ms = c.init_ms;
+        for (size_t i = 0; i < c.log.size() && i < cap; ++i) {
+            const CommRec& r = c.log[i];
+            if (ops) ops[i] = r.op;
+            if (bytes) bytes[i] = r.bytes;
+            if (roots) roots[i] = r.root;
+            if (ms) ms[i] = r.ms;
+            if (tags) tags[i] = r.tag.c_str();
+        }
+    });
+}
+
 int lsp_ctx_detach_comm(lsp_ctx* ctx) {
     return guarded(ctx, [&] {
         LSP_REQUIRE(ctx, LSP_E_ARG, "null ctx");
@@ -946,6 +979,8 @@ int lsp_proof_serialize(const lsp_proof* p, uint8_t* buf, size_t cap, size_t* le
         const std::vector<uint8_t>& b = p->wire;
         *len = b.size();
         if (buf) {
+            LSP_REQUIRE(!p->rehearsal, LSP_E_STATE,
+                        "a rehearsal (loopback) proof is not a proof: only its size can be queried");
             LSP_REQUIRE(cap >= b.size(), LSP_E_ARG, "buffer too small");
             std::memcpy(buf, b.data(), b.size());
         }
@@ -963,6 +998,7 @@ int lsp_proof_deserialize(const uint8_t* buf, size_t len, lsp_proof** out) {
 int lsp_proof_get_view(const lsp_proof* p, lsp_proof_view* view) {
     return guarded(nullptr, [&] {
         LSP_REQUIRE(p && view, LSP_E_ARG, "null");
+        LSP_REQUIRE(!p->rehearsal, LSP_E_STATE, "a rehearsal (loopback) proof is not a proof");
         proof_view(*p, view);
     });
 }

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
+#include <cstdint>
+#include <string>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -24,36 +26,119 @@
 
 namespace lsp {
 
+// One collective of a proof, as the communicator's log keeps it
+// (lsp_comm_log): op 'A' allgather (bytes = each rank's share) or 'B'
+// broadcast (bytes = the buffer, root), what it carried, and the device time
+// between events recorded on the context's stream around it -- the wait for
+// the slowest peer included
+struct CommRec {
+    char op;
+    size_t bytes;
+    int root;
+    std::string tag;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    double ms = -1;
+};
+
 struct Comm {
     int rank = 0, size = 1;
-    virtual ~Comm() {}
+    double init_ms = 0;          // communicator creation (RCCL: ncclCommInitRank), wall ms
+    std::vector<CommRec> log;    // the collectives since the last begin_log()
+    virtual ~Comm() {
+        for (CommRec& r : log) {
+            if (r.e0) (void)hipEventDestroy(r.e0);
+            if (r.e1) (void)hipEventDestroy(r.e1);
+        }
+    }
     // LoopbackComm: peers' data is fabricated, so the proof's self-checks
     // (the FRI final polynomial's degree) cannot hold and are skipped
     virtual bool rehearsal() const { return false; }
     // recv[r * bytes ...] = rank r's send (device buffers, ordered on ctx->stream)
-    virtual void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) = 0;
+    void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes, const char* tag = "") {
+        const size_t k = rec_begin(ctx, 'A', bytes, -1, tag);
+        do_allgather(ctx, send, recv, bytes);
+        rec_end(ctx, k);
+    }
     // every rank's buf = root's buf (device buffer)
-    virtual void bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) = 0;
+    void bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root, const char* tag = "") {
+        const size_t k = rec_begin(ctx, 'B', bytes, root, tag);
+        do_bcast(ctx, buf, bytes, root);
+        rec_end(ctx, k);
+    }
+    // a new proof: drop the previous log (its events go back to the context's pool)
+    void begin_log(lsp_ctx* ctx) {
+        for (CommRec& r : log) {
+            if (r.e0) ctx->event_pool.push_back(r.e0);
+            if (r.e1) ctx->event_pool.push_back(r.e1);
+        }
+        log.clear();
+    }
+    // the device times of the logged collectives (waits for the last event)
+    void resolve_log() {
+        for (CommRec& r : log) {
+            if (r.ms >= 0 || !r.e0 || !r.e1) continue;
+            float ms = 0;
+            LSP_HIP(hipEventSynchronize(r.e1));
+            LSP_HIP(hipEventElapsedTime(&ms, r.e0, r.e1));
+            r.ms = ms;
+        }
+    }
 
     // host-vector conveniences over the device collectives
-    std::vector<Fr> allgather_fr(lsp_ctx* ctx, const Fr* host, size_t n) {
+    std::vector<Fr> allgather_fr(lsp_ctx* ctx, const Fr* host, size_t n, const char* tag = "") {
         Fr* s = ctx->fbuf("comm_send", n);
         Fr* r = ctx->fbuf("comm_recv", n * (size_t)size);
         LSP_HIP(hipMemcpyAsync(s, host, n * sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
-        allgather(ctx, s, r, n * sizeof(Fr));
+        allgather(ctx, s, r, n * sizeof(Fr), tag);
         std::vector<Fr> out(n * (size_t)size);
         LSP_HIP(hipMemcpyAsync(out.data(), r, out.size() * sizeof(Fr), hipMemcpyDeviceToHost, ctx->stream));
         LSP_HIP(hipStreamSynchronize(ctx->stream));
         return out;
     }
+
+  protected:
+    virtual void do_allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) = 0;
+    virtual void do_bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) = 0;
+    // SoloComm (one rank) keeps no log: its "collectives" are local copies
+    virtual bool logs() const { return size > 1; }
+
+  private:
+    hipEvent_t take_event(lsp_ctx* ctx) {
+        hipEvent_t e;
+        if (!ctx->event_pool.empty()) {
+            e = ctx->event_pool.back();
+            ctx->event_pool.pop_back();
+        } else {
+            LSP_HIP(hipEventCreate(&e));
+        }
+        return e;
+    }
+    size_t rec_begin(lsp_ctx* ctx, char op, size_t bytes, int root, const char* tag) {
+        if (!logs() || log.size() >= 4096) return SIZE_MAX;
+        CommRec r;
+        r.op = op;
+        r.bytes = bytes;
+        r.root = root;
+        r.tag = tag ? tag : "";
+        r.e0 = take_event(ctx);
+        LSP_HIP(hipEventRecord(r.e0, ctx->stream));
+        log.push_back(std::move(r));
+        return log.size() - 1;
+    }
+    void rec_end(lsp_ctx* ctx, size_t k) {
+        if (k == SIZE_MAX) return;
+        log[k].e1 = take_event(ctx);
+        LSP_HIP(hipEventRecord(log[k].e1, ctx->stream));
+    }
 };
 
 struct SoloComm : Comm {
-    void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
+  protected:
+    void do_allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
         if (send != recv)
             LSP_HIP(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, ctx->stream));
     }
-    void bcast(lsp_ctx*, void*, size_t, int) override {}
+    void do_bcast(lsp_ctx*, void*, size_t, int) override {}
 };
 
 // Rehearsal of ONE rank of a G-rank proof on one GPU (lsp_ctx_attach_loopback):
@@ -68,16 +153,18 @@ struct LoopbackComm : Comm {
         rank = r;
         size = n;
     }
-    void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
+    bool rehearsal() const override { return true; }
+
+  protected:
+    void do_allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
         for (int r = 0; r < size; ++r) {
             void* dst = (char*)recv + (size_t)r * bytes;
             if (dst != send) LSP_HIP(hipMemcpyAsync(dst, send, bytes, hipMemcpyDeviceToDevice, ctx->stream));
         }
     }
-    void bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) override {
+    void do_bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) override {
         if (root != rank) LSP_HIP(hipMemsetAsync(buf, 0, bytes, ctx->stream));
     }
-    bool rehearsal() const override { return true; }
 };
 
 // Shared state of an in-process group: a generation barrier that any rank can
@@ -118,7 +205,9 @@ struct ThreadComm : Comm {
         rank = r;
         size = g->size;
     }
-    void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
+
+  protected:
+    void do_allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
         LSP_HIP(hipStreamSynchronize(ctx->stream));  // send is complete
         grp->slot[rank] = send;
         grp->barrier();
@@ -132,7 +221,7 @@ struct ThreadComm : Comm {
         LSP_HIP(hipStreamSynchronize(ctx->stream));
         grp->barrier();  // peers may reuse their send buffers only after every copy
     }
-    void bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) override {
+    void do_bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) override {
         LSP_HIP(hipStreamSynchronize(ctx->stream));
         if (rank == root) grp->slot[root] = buf;
         grp->barrier();

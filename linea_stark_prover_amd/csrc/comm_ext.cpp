@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -29,7 +30,9 @@ struct CallbackComm : Comm {
         rank = o.rank;
         size = o.size;
     }
-    void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
+
+  protected:
+    void do_allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
         hs.resize(bytes);
         hr.resize(bytes * (size_t)size);
         LSP_HIP(hipMemcpyAsync(hs.data(), send, bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -39,7 +42,7 @@ struct CallbackComm : Comm {
         LSP_HIP(hipMemcpyAsync(recv, hr.data(), hr.size(), hipMemcpyHostToDevice, ctx->stream));
         LSP_HIP(hipStreamSynchronize(ctx->stream));
     }
-    void bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) override {
+    void do_bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) override {
         hs.resize(bytes);
         if (rank == root) {
             LSP_HIP(hipMemcpyAsync(hs.data(), buf, bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -100,7 +103,9 @@ struct RcclComm : Comm {
     RcclComm(const ncclUniqueId& id, int r, int n) {
         rank = r;
         size = n;
+        const auto t0 = std::chrono::steady_clock::now();
         LSP_RCCL(rccl().init_rank(&comm, n, id, r));
+        init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     ~RcclComm() override {
         if (comm) rccl().destroy(comm);
@@ -116,12 +121,14 @@ struct RcclComm : Comm {
         count = bytes;
         return ncclUint8;
     }
-    void allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
+
+  protected:
+    void do_allgather(lsp_ctx* ctx, const void* send, void* recv, size_t bytes) override {
         size_t n;
         const ncclDataType_t t = dtype(bytes, n);
         LSP_RCCL(rccl().all_gather(send, recv, n, t, comm, ctx->stream));
     }
-    void bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) override {
+    void do_bcast(lsp_ctx* ctx, void* buf, size_t bytes, int root) override {
         constexpr size_t piece = (size_t)1 << 30;
         for (size_t off = 0; off < bytes; off += piece) {
             size_t n;

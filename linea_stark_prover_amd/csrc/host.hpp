@@ -118,12 +118,23 @@ struct P2Host {
     }
 };
 
+// The transcript conventions of include/lsp.h's lsp_params (U7, U8, U12),
+// each a named switch; the defaults are SURVEY 8(c)'s
+struct TranscriptCfg {
+    bool log_degree = true;      // U7: observe log2(h) first
+    bool public_values = true;   // U7: observe the public values before alpha
+    bool opened_values = false;  // U7: observe the opened values before alpha_fri
+    bool mont_bits = false;      // U8: sample_bits from the Montgomery form
+    bool final_poly = true;      // U12: observe the final polynomial
+};
+
 // HashChallenger<Val, Hash, 1> (bin/src/config.rs:23): input buffer,
 // output buffer, hash_iter on flush with the output chained back as input.
 struct Challenger {
     const P2Host* p2;
     std::vector<Fr> in, out;
-    explicit Challenger(const P2Host* p) : p2(p) {}
+    bool mont_bits = false;  // U8 (TranscriptCfg::mont_bits)
+    explicit Challenger(const P2Host* p, bool mont = false) : p2(p), mont_bits(mont) {}
     void observe(const Fr& x) {
         out.clear();
         in.push_back(x);
@@ -138,9 +149,10 @@ struct Challenger {
         out.pop_back();
         return r;
     }
-    // U8: low bits of the canonical value
+    // U8: low bits of the canonical value (mont_bits: of the Montgomery form)
     uint64_t sample_bits(uint32_t bits) {
-        Fr c = fr_to_canonical(sample());
+        const Fr s = sample();
+        const Fr c = mont_bits ? s : fr_to_canonical(s);
         uint64_t lo = (uint64_t)c.v[0] | ((uint64_t)c.v[1] << 32);
         return bits >= 64 ? lo : (lo & ((1ull << bits) - 1));
     }
@@ -191,6 +203,9 @@ struct lsp_proof {
     lsp::Fr troot, qroot, pow_w;
     std::vector<lsp::Fr> tl, tn, qc, roots, final_poly;
     std::vector<lsp::lsp_query> queries;
+    // made under a rehearsal transport (lsp_ctx_attach_loopback): peers' data
+    // fabricated, so not a proof -- serialize / view refuse it (shape queries only)
+    bool rehearsal = false;
     // caches filled on first use by calls that take a const proof (a proof may
     // be shared across threads, e.g. rayon tasks): built under cache_mu
     mutable std::mutex cache_mu;
@@ -263,6 +278,7 @@ struct lsp_ctx {
     lsp::F29* rc29_dev = nullptr; // the same in the 29-bit-limb form the hash kernels use
     uint32_t log_blowup = 3, log_final_poly_len = 0, num_queries = 33, pow_bits = 0;
     int32_t public_degree = 1;
+    lsp::TranscriptCfg transcript;  // U7/U8/U12 (lsp_params)
     std::string err;
     std::mutex mu;
     struct Buf {

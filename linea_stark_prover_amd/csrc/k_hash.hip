@@ -144,11 +144,12 @@ __global__ __launch_bounds__(256) void k_merkle_top(Fr* __restrict__ layers, siz
 // PoW grinding (GrindingChallenger::grind, [EXT p3-challenger]; U8): each lane
 // tests candidate witnesses w: the sponge state before the block holding w is
 // fixed (host), w is absorbed into lane `wlane` (the other rate lane keeps
-// `other`), one permutation, then the low `bits` of the canonical s0 must be 0.
+// `other`), one permutation, then the low `bits` of the canonical s0 (mont:
+// of its Montgomery form, U8's switch) must be 0.
 // The smallest hit of the batch is kept with an atomic min.
 template <uint32_t D>
 __global__ __launch_bounds__(256) void k_grind(Fr pre0, Fr pre1, Fr pre2, uint32_t wlane, uint64_t base,
-                                               uint64_t count, uint32_t bits, const F29* __restrict__ rc,
+                                               uint64_t count, uint32_t bits, uint32_t mont, const F29* __restrict__ rc,
                                                uint32_t rf, uint32_t rp, unsigned long long* __restrict__ best) {
     __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
     f29_qtab_init(qt);
@@ -161,7 +162,8 @@ __global__ __launch_bounds__(256) void k_grind(Fr pre0, Fr pre1, Fr pre2, uint32
         const F29 fw = f29_from_fr(fr_from_u64(w));
         F29 s0 = wlane == 0 ? fw : c0, s1 = wlane == 0 ? c1 : fw, s2 = c2;
         permute3_any<D, 1>(s0, s1, s2, rc, rf, rp, qt);
-        const Fr c = fr_to_canonical(f29_to_fr(s0));
+        const Fr m = f29_to_fr(s0);  // Montgomery form, reduced
+        const Fr c = mont ? m : fr_to_canonical(m);
         const uint64_t lo = (uint64_t)c.v[0] | ((uint64_t)c.v[1] << 32);
         if ((lo & mask) == 0) atomicMin(best, (unsigned long long)w);
     }
@@ -308,10 +310,11 @@ hipError_t launch_calib_perm(Fr* out, size_t nthreads, uint32_t iters, const F29
     return hipGetLastError();
 }
 
-hipError_t launch_grind(const Fr pre[3], uint32_t wlane, uint64_t base, uint64_t count, uint32_t bits,
+hipError_t launch_grind(const Fr pre[3], uint32_t wlane, uint64_t base, uint64_t count, uint32_t bits, bool mont,
                         const F29* rc, P2Layout L, unsigned long long* best, hipStream_t st) {
     const unsigned blocks = 256 * 16;
-    LSP_DISPATCH_D(L, k_grind, dim3(blocks), dim3(256), 0, st, pre[0], pre[1], pre[2], wlane, base, count, bits, rc,
+    LSP_DISPATCH_D(L, k_grind, dim3(blocks), dim3(256), 0, st, pre[0], pre[1], pre[2], wlane, base, count, bits,
+                   (uint32_t)mont, rc,
                    L.rounds_f, L.rounds_p, best);
     return hipGetLastError();
 }

@@ -113,8 +113,9 @@ hipError_t launch_fold_hash(const FoldSpec& f, size_t nleaves, Fr* out, const F2
 hipError_t launch_hash_rows(const MatList& m, size_t nrows, Fr* out, const F29* rc29, P2Layout L, hipStream_t st);
 // dst[i] = compress(src[2i], src[2i+1]) for i < nout
 hipError_t launch_merkle_level(const Fr* src, Fr* dst, size_t nout, const F29* rc29, P2Layout L, hipStream_t st);
-// PoW grinding: test witnesses [base, base+count); *best = min hit (caller inits to ~0)
-hipError_t launch_grind(const Fr pre[3], uint32_t wlane, uint64_t base, uint64_t count, uint32_t bits,
+// PoW grinding: test witnesses [base, base+count); *best = min hit (caller inits to ~0);
+// mont: sample_bits from the Montgomery form (U8)
+hipError_t launch_grind(const Fr pre[3], uint32_t wlane, uint64_t base, uint64_t count, uint32_t bits, bool mont,
                         const F29* rc29, P2Layout L, unsigned long long* best, hipStream_t st);
 // full tree above the leaf digests already stored at layers[0..nleaves)
 hipError_t launch_merkle_tree(Fr* layers, size_t nleaves, const F29* rc29, P2Layout L, hipStream_t st);

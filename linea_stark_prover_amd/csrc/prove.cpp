@@ -628,7 +628,7 @@ uint64_t grind_device(lsp_ctx* ctx, Challenger& ch, uint32_t bits) {
     const uint64_t batch = 1ull << 22;
     for (uint64_t base = 0;; base += batch) {
         LSP_HIP(hipMemsetAsync(best, 0xff, sizeof(unsigned long long), ctx->stream));
-        LSP_HIP(launch_grind(pre, wlane, base, batch, bits, ctx->rc29_dev, ctx->p2.L, best, ctx->stream));
+        LSP_HIP(launch_grind(pre, wlane, base, batch, bits, ch.mont_bits, ctx->rc29_dev, ctx->p2.L, best, ctx->stream));
         unsigned long long got = 0;
         LSP_HIP(hipMemcpyAsync(&got, best, sizeof(got), hipMemcpyDeviceToHost, ctx->stream));
         LSP_HIP(hipStreamSynchronize(ctx->stream));
@@ -644,12 +644,12 @@ uint64_t grind_device(lsp_ctx* ctx, Challenger& ch, uint32_t bits) {
 // Root of a Merkle tree whose 2^b bottom subtrees live on the 2^b ranks
 // (rank r's subtree root = `local`, leaves r*S .. (r+1)*S - 1).  `top` gets
 // the b + 1 host layers above the subtrees (top[0] = the rank roots).
-static Fr shard_root(lsp_ctx* ctx, Comm& comm, const Fr& local, std::vector<std::vector<Fr>>& top) {
+static Fr shard_root(lsp_ctx* ctx, Comm& comm, const Fr& local, std::vector<std::vector<Fr>>& top, const char* tag) {
     if (comm.size == 1) {
         top.assign(1, std::vector<Fr>(1, local));
         return local;
     }
-    top.assign(1, comm.allgather_fr(ctx, &local, 1));
+    top.assign(1, comm.allgather_fr(ctx, &local, 1, tag));
     while (top.back().size() > 1) {
         const std::vector<Fr>& lo = top.back();
         std::vector<Fr> up(lo.size() / 2);
@@ -674,6 +674,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
     LSP_REQUIRE(air.max_col < w, LSP_E_ARG, "AIR column id outside the trace width");
     const ActiveProof active;
     const DeferTopUploads defer(ctx);
+    comm.begin_log(ctx);
     const uint32_t log_h = log2_exact(h);
     LSP_REQUIRE(h >= 2, LSP_E_SIZE, "trace needs at least 2 rows");
     const uint32_t lb = ctx->log_blowup;
@@ -713,6 +714,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
     proof->log_h = log_h;
     proof->log_q = log_q;
     proof->w = (uint32_t)w;
+    proof->rehearsal = comm.rehearsal();
     try {
         T.begin("prove");
         // ---- commit to trace data
@@ -735,7 +737,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             m.c0 = (uint32_t)host_bitrev(g, b);
             m.cstep = G;
             LSP_HIP(launch_intt(d_trace, m, xl, cg, log_h, ctx->twiddle29(log_h, true), st));
-            comm.allgather(ctx, xl, coef, h * cg * sizeof(Fr));
+            comm.allgather(ctx, xl, coef, h * cg * sizeof(Fr), "trace coefficients");
             tcoef = coef;
             tmap = ColMap::blocked(b, cg);
         } else if (sub) {  // every rank inverts every column (LSP_SHARD_SPLIT_INTT=0)
@@ -754,14 +756,18 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         Fr* tlay = ctx->fbuf("t_tree", 2 * S - 1);
         std::vector<std::vector<Fr>> ttop, qtop;
         T.begin("merkle tree");
-        proof->troot = shard_root(ctx, comm, commit_device(ctx, one_mat(lde, (uint32_t)w), S, tlay), ttop);
+        proof->troot = shard_root(ctx, comm, commit_device(ctx, one_mat(lde, (uint32_t)w), S, tlay), ttop,
+                                  "trace subtree roots");
         T.end("merkle tree");
         T.end("commit to trace data");
 
-        Challenger ch(&ctx->p2);
-        ch.observe(fr_from_u64(log_h));
+        // U7: the instance, then the quotient challenge (TranscriptCfg switches)
+        const TranscriptCfg& TC = ctx->transcript;
+        Challenger ch(&ctx->p2, TC.mont_bits);
+        if (TC.log_degree) ch.observe(fr_from_u64(log_h));
         ch.observe(proof->troot);
-        for (size_t i = 0; i < npub; ++i) ch.observe(pub[i]);
+        if (TC.public_values)
+            for (size_t i = 0; i < npub; ++i) ch.observe(pub[i]);
         const Fr alpha = ch.sample();
 
         // ---- quotient.  Point i reads LDE rows bitrev_Q(i) and bitrev_Q(i + q):
@@ -862,7 +868,9 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             if (qsplit && g < Gq)
                 LSP_HIP(launch_intt(qloc, ColMap::plain((uint32_t)cpr), stage + (size_t)g * Sq, cpr, log_h,
                                     ctx->twiddle29(log_h, true), st));
-            for (uint32_t r = 0; r < Gq; ++r) comm.bcast(ctx, stage + (size_t)r * Sq, Sq * sizeof(Fr), (int)r);
+            for (uint32_t r = 0; r < Gq; ++r)
+                comm.bcast(ctx, stage + (size_t)r * Sq, Sq * sizeof(Fr), (int)r,
+                           qsplit ? "quotient chunk coefficients" : "quotient values");
             if (!qsplit) LSP_HIP(launch_assemble_chunks(stage, logGq, Sq, qv, st));
         }
         T.end("compute quotient polynomial");
@@ -891,15 +899,17 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         }
         T.end("coset_lde_batch (quotient)");
         Fr* qlay = ctx->fbuf("q_tree", 2 * S - 1);
-        proof->qroot = shard_root(ctx, comm, commit_device(ctx, one_mat(qlde, (uint32_t)q), S, qlay), qtop);
+        proof->qroot = shard_root(ctx, comm, commit_device(ctx, one_mat(qlde, (uint32_t)q), S, qlay), qtop,
+                                  "quotient subtree roots");
         T.end("commit to quotient poly chunks");
         ch.observe(proof->qroot);
         const Fr zeta = ch.sample();
         const Fr zeta_next = fr_mul(zeta, wh);
 
-        // ---- open
+        // ---- open (alpha_fri is sampled once the opened values exist: U7 may
+        // observe them first; the default samples it right after zeta, and
+        // nothing touches the transcript in between)
         T.begin("open");
-        const Fr alpha_fri = ch.sample();
         T.begin("compute_inverse_denominators");
         uint32_t L1N;
         const Fr* tabN = pow_table(ctx, "tabN", host_two_adic_generator(logN), logN, L1N);
@@ -976,7 +986,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             for (size_t k = 0; k < jw[j]; ++k) hs[joff[j] + k] = job_here[j] ? fr_mul(hs[joff[j] + k], f) : fr_zero();
         }
         if (G > 1) {  // every value from its job's rank(s): the sum over ranks
-            const std::vector<Fr> all = comm.allgather_fr(ctx, hs, nsum);
+            const std::vector<Fr> all = comm.allgather_fr(ctx, hs, nsum, "opened values");
             for (size_t k = 0; k < nsum; ++k) {
                 Fr acc = fr_zero();
                 for (uint32_t r = 0; r < G; ++r) acc = fr_add(acc, all[(size_t)r * nsum + k]);
@@ -987,6 +997,12 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         proof->tn.assign(hs + w, hs + 2 * w);
         proof->qc.assign(hs + 2 * w, hs + 2 * w + q);
         T.end("compute opened values with Lagrange interpolation");
+        if (TC.opened_values) {  // U7: every opened value, in (matrix, point) order, before alpha_fri
+            for (const Fr& v : proof->tl) ch.observe(v);
+            for (const Fr& v : proof->tn) ch.observe(v);
+            for (const Fr& v : proof->qc) ch.observe(v);
+        }
+        const Fr alpha_fri = ch.sample();
 
         T.begin("reduce rows");
         // the (matrix, point) order of TwoAdicFriPcs::open that the reduction
@@ -1050,7 +1066,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         auto replicate = [&]() {  // gather the short vector to every rank
             const size_t loc = len >> b;
             Fr* rep = ctx->fbuf("f_rep", 2 * len);
-            comm.allgather(ctx, fv + vo, rep, loc * sizeof(Fr));
+            comm.allgather(ctx, fv + vo, rep, loc * sizeof(Fr), "FRI vector");
             fv = rep;
             vo = 0;
             sharded = false;
@@ -1174,7 +1190,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             R.sharded = sharded;
             const Fr lroot = commit_device(ctx, one_mat(fv + vo, 2), ml, ftree + to, pending ? &pend : nullptr);
             pending = false;
-            const Fr root = sharded ? shard_root(ctx, comm, lroot, R.top) : lroot;
+            const Fr root = sharded ? shard_root(ctx, comm, lroot, R.top, "FRI subtree roots") : lroot;
             proof->roots.push_back(root);
             ch.observe(root);
             const Fr beta = ch.sample();
@@ -1232,7 +1248,8 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                 else  // (a rehearsal rank's fabricated peer data folds to no polynomial: not checked)
                     LSP_REQUIRE(fr_is_zero(acc) || comm.rehearsal(), LSP_E_STATE, "FRI final polynomial degree too high");
             }
-            for (const Fr& c : proof->final_poly) ch.observe(c);
+            if (TC.final_poly)  // U12
+                for (const Fr& c : proof->final_poly) ch.observe(c);
         }
         T.begin("grind for proof-of-work witness");
         proof->pow_w = fr_from_u64(grind_device(ctx, ch, ctx->pow_bits));
@@ -1293,7 +1310,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                 std::copy(got + k * E, got + (k + 1) * E, slots.begin() + (size_t)mine[k] * E);
         }
         const auto q2 = std::chrono::steady_clock::now();
-        const std::vector<Fr> all = G > 1 ? comm.allgather_fr(ctx, slots.data(), slots.size()) : slots;
+        const std::vector<Fr> all = G > 1 ? comm.allgather_fr(ctx, slots.data(), slots.size(), "query openings") : slots;
         auto top_path = [&](const std::vector<std::vector<Fr>>& top, size_t sub, std::vector<Fr>& out) {
             for (uint32_t i = 0; i + 1 < top.size(); ++i) out.push_back(top[i][(sub >> i) ^ 1]);
         };

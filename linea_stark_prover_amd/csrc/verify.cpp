@@ -78,21 +78,29 @@ int verify_host(const lsp_ctx* ctx, const Air& air, const Fr* pub, size_t npub, 
     const Fr pw = r.fr();
     if (r.bad) return 5;
     const Fr one = fr_one(), GEN = host_generator();
-    Challenger ch(&ctx->p2);
-    ch.observe(fr_from_u64(log_h));
+    const TranscriptCfg& TC = ctx->transcript;  // U7 / U8 / U12, as the prover
+    Challenger ch(&ctx->p2, TC.mont_bits);
+    if (TC.log_degree) ch.observe(fr_from_u64(log_h));
     ch.observe(troot);
-    for (size_t i = 0; i < npub; ++i) ch.observe(pub[i]);
+    if (TC.public_values)
+        for (size_t i = 0; i < npub; ++i) ch.observe(pub[i]);
     const Fr alpha = ch.sample();
     ch.observe(qroot);
     const Fr zeta = ch.sample();
     const Fr wh = host_two_adic_generator(log_h), wh_inv = fr_inv(wh);
     const Fr zeta_next = fr_mul(zeta, wh);
+    if (TC.opened_values) {
+        for (const Fr& v : tl) ch.observe(v);
+        for (const Fr& v : tn) ch.observe(v);
+        for (const Fr& v : qc) ch.observe(v);
+    }
     const Fr alpha_fri = ch.sample();
     for (uint32_t k = 0; k < nr; ++k) {
         ch.observe(roots[k]);
         betas[k] = ch.sample();
     }
-    for (auto& c : fp) ch.observe(c);
+    if (TC.final_poly)
+        for (auto& c : fp) ch.observe(c);
     const Fr pwc = fr_to_canonical(pw);
     for (int i = 2; i < 8; ++i)
         if (pwc.v[i]) return 6;

@@ -31,6 +31,22 @@ import numpy as np
 from . import _lib as L
 
 
+def wire_size(log_h: int, w: int, log_q: int, log_blowup: int = 3, log_final_poly_len: int = 0,
+              num_queries: int = 33) -> int:
+    """Bytes of a serialized proof (csrc/proof.cpp serialize) of an h x w
+    trace with 2^log_q quotient chunks: header, commitments, opened values,
+    FRI roots and final polynomial, pow witness, then per query the trace and
+    quotient rows with their paths and, per FRI round r, the sibling and a
+    path of log N - 1 - r digests (each path prefixed by its u32 length)."""
+    logN = log_h + log_blowup
+    nr = logN - log_blowup - log_final_poly_len
+    q = 1 << log_q
+    per_query_fr = w + logN + q + logN + nr + sum(logN - 1 - r for r in range(nr))
+    nfr = 3 + 2 * w + q + nr + (1 << log_final_poly_len) + num_queries * per_query_fr
+    nu32 = 6 + num_queries * (2 + nr)
+    return 8 + 4 * nu32 + 32 * nfr
+
+
 class LspProofView(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint32) for n in ("degree_bits", "log_quotient_chunks", "width", "num_queries",
                                                 "num_fri_rounds", "final_poly_len", "input_path_len")] + \

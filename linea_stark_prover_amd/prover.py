@@ -56,6 +56,12 @@ class StarkConfig:
     # None = the default layer (internal diag (1, 1, 2); external circ(2, 1, 1))
     internal_diag: Optional[Tuple[int, int, int]] = None
     external_mds: Optional[Tuple[int, ...]] = None   # 9 entries, row-major
+    # U7/U8/U12 transcript conventions (include/lsp.h lsp_params), 0/False = default
+    skip_log_degree: bool = False         # U7: log2(h) not observed
+    skip_public_values: bool = False      # U7: [alpha, delta] not observed before the quotient challenge
+    observe_opened_values: bool = False   # U7: opened values observed before alpha_fri
+    sample_bits_montgomery: bool = False  # U8: sample_bits from the Montgomery form
+    skip_final_poly: bool = False         # U12: final polynomial not observed
 
     def seeded(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """(alpha, delta, round_constants) from the documented seeded generator."""
@@ -65,11 +71,14 @@ class StarkConfig:
         return a, d, rc
 
 
-def _take_proof(proof: ctypes.c_void_p) -> bytes:
-    """serialize and free an lsp_proof handle"""
+def _take_proof(proof: ctypes.c_void_p, size_only: bool = False):
+    """serialize and free an lsp_proof handle (size_only: its wire size, the
+    one thing a rehearsal proof answers)"""
     try:
         n = ctypes.c_size_t()
         L.check(L.lib().lsp_proof_serialize(proof, None, 0, ctypes.byref(n)))
+        if size_only:
+            return n.value
         buf = ctypes.create_string_buffer(n.value)
         L.check(L.lib().lsp_proof_serialize(proof, buf, n.value, ctypes.byref(n)))
         return buf.raw[:n.value]
@@ -91,10 +100,13 @@ class Context:
         self._mds = None if config.external_mds is None else to_mont(config.external_mds)
         assert self._diag is None or self._diag.shape[0] == 3, "internal_diag needs 3 entries"
         assert self._mds is None or self._mds.shape[0] == 9, "external_mds needs 9 entries"
-        p = L.LspParams(config.sbox_degree, config.rounds_f, config.rounds_p, _ptr(self._rc), config.log_blowup,
-                        config.log_final_poly_len, config.num_queries, config.proof_of_work_bits,
-                        config.public_degree, None if self._diag is None else _ptr(self._diag),
-                        None if self._mds is None else _ptr(self._mds))
+        p = L.LspParams(sbox_degree=config.sbox_degree, rounds_f=config.rounds_f, rounds_p=config.rounds_p,
+                        round_constants=_ptr(self._rc), log_blowup=config.log_blowup,
+                        log_final_poly_len=config.log_final_poly_len, num_queries=config.num_queries,
+                        proof_of_work_bits=config.proof_of_work_bits, public_degree=config.public_degree,
+                        internal_diag=None if self._diag is None else _ptr(self._diag),
+                        external_mds=None if self._mds is None else _ptr(self._mds),
+                        **{k: int(getattr(config, k)) for k in L.TRANSCRIPT_SWITCHES})
         h = ctypes.c_void_p()
         L.check(L.lib().lsp_ctx_create(device, ctypes.byref(p), ctypes.byref(h)))
         self.h = h
@@ -121,6 +133,23 @@ class Context:
 
     def synchronize(self):
         self._chk(L.lib().lsp_synchronize(self.h))
+
+    def comm_log(self):
+        """the attached communicator's collectives of the last sharded proof
+        (lsp_comm_log): (entries, init_ms), each entry a dict with op
+        ("allgather" / "bcast"), bytes, root, tag and device ms"""
+        n, init = ctypes.c_size_t(), ctypes.c_double()
+        self._chk(L.lib().lsp_comm_log(self.h, None, None, None, None, None, 0, ctypes.byref(n),
+                                       ctypes.byref(init)))
+        k = n.value
+        ops = ctypes.create_string_buffer(max(k, 1))
+        nb, roots = (ctypes.c_size_t * max(k, 1))(), (ctypes.c_int * max(k, 1))()
+        ms, tags = (ctypes.c_double * max(k, 1))(), (ctypes.c_char_p * max(k, 1))()
+        self._chk(L.lib().lsp_comm_log(self.h, ops, nb, roots, ms, tags, k, ctypes.byref(n), ctypes.byref(init)))
+        out = [{"op": "allgather" if ops.raw[i:i + 1] == b"A" else "bcast", "bytes": int(nb[i]),
+                "root": None if roots[i] < 0 else int(roots[i]), "tag": tags[i].decode(), "ms": float(ms[i])}
+               for i in range(min(k, n.value))]
+        return out, float(init.value)
 
     # ---------------------------------------------------------- device buffers
     def dev_alloc(self, nbytes: int) -> int:

@@ -43,6 +43,14 @@ class Dist:
         self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
         return float(t.item())
 
+    def all_gather_object(self, obj) -> list:
+        """every rank's `obj`, in rank order (the control group; small objects)"""
+        if self.pg is None:
+            return [obj]
+        out = [None] * self.world
+        self.pg.all_gather_object(out, obj)
+        return out
+
     def close(self):
         if self.pg is not None:
             self.pg.destroy_process_group()

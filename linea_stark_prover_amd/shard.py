@@ -123,9 +123,11 @@ def detach(ctx: Context) -> None:
 
 
 def prove_sharded(ctx: Context, trace, air: LineaAIR, public_values: np.ndarray, h: Optional[int] = None,
-                  w: Optional[int] = None) -> bytes:
+                  w: Optional[int] = None, size_only: bool = False):
     """This rank's part of a sharded proof; every rank returns the whole proof.
-    `trace`: (h, w, 4) host array or a device pointer (int) with h and w."""
+    `trace`: (h, w, 4) host array or a device pointer (int) with h and w.
+    size_only: return the proof's wire size instead (a rehearsal proof under
+    lsp_ctx_attach_loopback answers nothing else)."""
     desc = (ctypes.c_int32 * len(air.descriptor()))(*air.descriptor())
     pub = _fr_arr(public_values).reshape(-1, 4)
     proof = ctypes.c_void_p()
@@ -140,4 +142,4 @@ def prove_sharded(ctx: Context, trace, air: LineaAIR, public_values: np.ndarray,
     if rc != L.LSP_OK and comm is not None and comm.error is not None:
         raise RuntimeError(f"communicator failed: {comm.error!r}") from comm.error
     ctx._chk(rc)
-    return _take_proof(proof)
+    return _take_proof(proof, size_only)

@@ -29,7 +29,8 @@ class Params(ctypes.Structure):
 
 class Fri(ctypes.Structure):
     _fields_ = [("log_blowup", ctypes.c_uint32), ("log_final_poly_len", ctypes.c_uint32),
-                ("num_queries", ctypes.c_uint32), ("pow_bits", ctypes.c_uint32)]
+                ("num_queries", ctypes.c_uint32), ("pow_bits", ctypes.c_uint32),
+                ("transcript", ctypes.c_uint32)]  # LO_T_* mask (U7/U8/U12), 0 = defaults
 
 
 class Debug(ctypes.Structure):
@@ -139,7 +140,7 @@ def setup(seed: int = O.DEFAULT_SEED, sbox_degree=11, rounds_f=8, rounds_p=22, i
 
 
 def fri_params(fp: O.FriParams = O.FriParams()) -> Fri:
-    return Fri(fp.log_blowup, fp.log_final_poly_len, fp.num_queries, fp.proof_of_work_bits)
+    return Fri(fp.log_blowup, fp.log_final_poly_len, fp.num_queries, fp.proof_of_work_bits, fp.transcript_bits())
 
 
 def gen_perm_trace(p: Params, log_n: int, ncols: int, seed: int = O.DEFAULT_SEED, small=False):

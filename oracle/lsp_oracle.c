@@ -774,8 +774,14 @@ typedef struct {
     size_t nin;
     lo_fr out[1];
     size_t nout;
+    int mont_bits; /* U8: sample_bits from the Montgomery form (LO_T_SAMPLE_BITS_MONT) */
 } chal_t;
-static void ch_init(chal_t *c, const lo_params *p) { c->p = p; c->nin = 0; c->nout = 0; }
+static void ch_init(chal_t *c, const lo_params *p, uint32_t transcript) {
+    c->p = p;
+    c->nin = 0;
+    c->nout = 0;
+    c->mont_bits = (transcript & LO_T_SAMPLE_BITS_MONT) != 0;
+}
 static void ch_observe(chal_t *c, const lo_fr *x) {
     c->nout = 0;
     if (c->nin < 4096) c->in[c->nin++] = *x;
@@ -794,7 +800,10 @@ static lo_fr ch_sample(chal_t *c) {
 static uint64_t ch_sample_bits(chal_t *c, uint32_t bits) {
     lo_fr s = ch_sample(c);
     uint64_t can[4];
-    lo_fr_to_canonical(&s, can);
+    if (c->mont_bits)
+        memcpy(can, s.l, sizeof can); /* lo_fr holds the reduced Montgomery form */
+    else
+        lo_fr_to_canonical(&s, can);
     return bits >= 64 ? can[0] : (can[0] & ((1ULL << bits) - 1));
 }
 static int ch_check_witness(chal_t *c, uint32_t bits, uint64_t w) {
@@ -986,12 +995,14 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
     lo_fr troot = tlay[2 * N - 2];
 
     chal_t *ch = (chal_t *)malloc(sizeof(chal_t));
-    ch_init(ch, p);
+    ch_init(ch, p, fri->transcript);
     lo_fr x = fu(log_h);
-    ch_observe(ch, &x);
+    if (!(fri->transcript & LO_T_SKIP_LOG_DEGREE)) ch_observe(ch, &x);
     ch_observe(ch, &troot);
-    ch_observe(ch, &p->alpha);
-    ch_observe(ch, &p->delta);
+    if (!(fri->transcript & LO_T_SKIP_PUBLIC)) {
+        ch_observe(ch, &p->alpha);
+        ch_observe(ch, &p->delta);
+    }
     lo_fr alpha = ch_sample(ch);
 
     /* ---- quotient */
@@ -1041,8 +1052,7 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
     lo_fr zeta = ch_sample(ch), zeta_next;
     fmul(&zeta, &wh, &zeta_next);
 
-    /* ---- open */
-    lo_fr alpha_fri = ch_sample(ch);
+    /* ---- open (alpha_fri is sampled after the opened values: U7) */
     lo_fr *xs = (lo_fr *)malloc(sizeof(lo_fr) * N), *xs_nat = (lo_fr *)malloc(sizeof(lo_fr) * N);
     powers(two_adic_gen(logN), N, xs_nat, nthreads);
     for (size_t i = 0; i < N; ++i) fmul(&GEN, &xs_nat[bitrev64(i, logN)], &xs[i]);
@@ -1062,6 +1072,12 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
     interpolate(lde, h, w, xs, invd_z, &zeta, ys_z);
     interpolate(lde, h, w, xs, invd_zn, &zeta_next, ys_zn);
     interpolate(qlde, h, q, xs, invd_z, &zeta, ys_q);
+    if (fri->transcript & LO_T_OBSERVE_OPENED) {
+        for (size_t c = 0; c < w; ++c) ch_observe(ch, &ys_z[c]);
+        for (size_t c = 0; c < w; ++c) ch_observe(ch, &ys_zn[c]);
+        for (size_t j = 0; j < q; ++j) ch_observe(ch, &ys_q[j]);
+    }
+    lo_fr alpha_fri = ch_sample(ch);
 
     size_t nap = 2 * w + q + 1;
     lo_fr *apw = (lo_fr *)malloc(sizeof(lo_fr) * nap);
@@ -1135,7 +1151,8 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
     for (size_t i = 0; i < len; ++i) fmul(&fin[i], &linv, &fin[i]);
     for (size_t i = flen; i < len; ++i)
         if (!fis_zero(&fin[i])) return -4; /* final poly degree too high */
-    for (size_t i = 0; i < flen; ++i) ch_observe(ch, &fin[i]);
+    if (!(fri->transcript & LO_T_SKIP_FINAL_POLY))
+        for (size_t i = 0; i < flen; ++i) ch_observe(ch, &fin[i]);
     uint64_t pw = ch_grind(ch, fri->pow_bits);
     if (cur != ro) free(cur);
 
@@ -1256,23 +1273,30 @@ int lo_verify(const lo_params *p, const lo_fri *fri, const int32_t *air, size_t 
     lo_fr fp = rd_fr(&r), pwf = rd_fr(&r);
     int rc = 0;
     chal_t *ch = (chal_t *)malloc(sizeof(chal_t));
-    ch_init(ch, p);
+    ch_init(ch, p, fri->transcript);
     lo_fr x = fu(log_h);
-    ch_observe(ch, &x);
+    if (!(fri->transcript & LO_T_SKIP_LOG_DEGREE)) ch_observe(ch, &x);
     ch_observe(ch, &troot);
-    ch_observe(ch, &p->alpha);
-    ch_observe(ch, &p->delta);
+    if (!(fri->transcript & LO_T_SKIP_PUBLIC)) {
+        ch_observe(ch, &p->alpha);
+        ch_observe(ch, &p->delta);
+    }
     lo_fr alpha = ch_sample(ch);
     ch_observe(ch, &qroot);
     lo_fr zeta = ch_sample(ch), wh = two_adic_gen(log_h), zeta_next, whinv;
     fmul(&zeta, &wh, &zeta_next);
     finv(&wh, &whinv);
+    if (fri->transcript & LO_T_OBSERVE_OPENED) {
+        for (uint32_t c = 0; c < w; ++c) ch_observe(ch, &tl[c]);
+        for (uint32_t c = 0; c < w; ++c) ch_observe(ch, &tn[c]);
+        for (size_t j = 0; j < q; ++j) ch_observe(ch, &qc[j]);
+    }
     lo_fr alpha_fri = ch_sample(ch);
     for (uint32_t k = 0; k < nr; ++k) {
         ch_observe(ch, &roots[k]);
         betas[k] = ch_sample(ch);
     }
-    ch_observe(ch, &fp);
+    if (!(fri->transcript & LO_T_SKIP_FINAL_POLY)) ch_observe(ch, &fp);
     uint64_t pwc[4];
     lo_fr_to_canonical(&pwf, pwc);
     if (pwc[1] | pwc[2] | pwc[3]) { rc = 4; goto done; }

@@ -39,8 +39,19 @@ typedef struct {
     lo_fr int_diag[3];
 } lo_params;
 
+/* transcript conventions (include/lsp.h lsp_params):
+ * lo_fri.transcript is an OR of these, 0 = the defaults */
+enum {
+    LO_T_SKIP_LOG_DEGREE = 1,    /* U7: log2(h) not observed */
+    LO_T_SKIP_PUBLIC = 2,        /* U7: public values not observed before alpha */
+    LO_T_OBSERVE_OPENED = 4,     /* U7: opened values observed before alpha_fri */
+    LO_T_SAMPLE_BITS_MONT = 8,   /* U8: sample_bits from the Montgomery form */
+    LO_T_SKIP_FINAL_POLY = 16    /* U12: final polynomial not observed */
+};
+
 typedef struct {
     uint32_t log_blowup, log_final_poly_len, num_queries, pow_bits;
+    uint32_t transcript;
 } lo_fri;
 
 /* field helpers */

@@ -353,10 +353,11 @@ def eval_poly(coeffs: List[int], x: int) -> int:
 # A16/A17 -- HashChallenger<Val, Hash, 1> (bin/src/config.rs:23) + U8
 # ---------------------------------------------------------------------------
 class HashChallenger:
-    def __init__(self, pp: Poseidon2Params, initial=None):
+    def __init__(self, pp: Poseidon2Params, initial=None, mont_bits: bool = False):
         self.pp = pp
         self.input_buffer = list(initial or [])
         self.output_buffer: List[int] = []
+        self.mont_bits = mont_bits  # U8 switch: sample_bits from the Montgomery form x * 2^256 mod r
 
     def observe(self, x: int):
         self.output_buffer.clear()
@@ -377,7 +378,10 @@ class HashChallenger:
         return self.output_buffer.pop()
 
     def sample_bits(self, bits: int) -> int:
-        return self.sample() & ((1 << bits) - 1)
+        x = self.sample()
+        if self.mont_bits:
+            x = x * MONT_R % P
+        return x & ((1 << bits) - 1)
 
     def check_witness(self, bits: int, witness: int) -> bool:
         self.observe(witness)
@@ -386,7 +390,7 @@ class HashChallenger:
     def grind(self, bits: int) -> int:
         w = 0
         while True:
-            probe = HashChallenger(self.pp)
+            probe = HashChallenger(self.pp, mont_bits=self.mont_bits)
             probe.input_buffer = list(self.input_buffer)
             probe.output_buffer = list(self.output_buffer)
             if probe.check_witness(bits, w):
@@ -695,6 +699,17 @@ class FriParams:
     log_final_poly_len: int = 0  # bin/src/main.rs:60
     num_queries: int = 33        # bin/src/main.rs:61
     proof_of_work_bits: int = 0  # bin/src/main.rs:62
+    # transcript conventions of the fork (include/lsp.h lsp_params), defaults first
+    observe_log_degree: bool = True       # U7: challenger.observe(log_degree)
+    observe_public_values: bool = True    # U7: observe_slice(public_values) before alpha
+    observe_opened_values: bool = False   # U7: opened values observed before alpha_fri
+    sample_bits_montgomery: bool = False  # U8: sample_bits from the Montgomery form
+    observe_final_poly: bool = True       # U12: final polynomial observed before grinding
+
+    def transcript_bits(self) -> int:
+        """the C oracle's lo_fri.transcript mask (LO_T_*)"""
+        return ((not self.observe_log_degree) * 1 | (not self.observe_public_values) * 2
+                | self.observe_opened_values * 4 | self.sample_bits_montgomery * 8 | (not self.observe_final_poly) * 16)
 
 
 def interpolate_coset(low_rows_bitrev: List[List[int]], shift: int, z: int) -> List[int]:
@@ -792,10 +807,12 @@ def prove(cfgs, trace_rows: List[List[int]], pub: List[int], pp: Poseidon2Params
     log["trace_lde"] = lde
     log["trace_layers"] = t_tree.layers
 
-    ch = HashChallenger(pp)
-    ch.observe(log_h)
+    ch = HashChallenger(pp, mont_bits=fri.sample_bits_montgomery)
+    if fri.observe_log_degree:
+        ch.observe(log_h)
     ch.observe(t_tree.root)
-    ch.observe_slice(pub)
+    if fri.observe_public_values:
+        ch.observe_slice(pub)
     alpha = ch.sample()
     log["alpha"] = alpha
 
@@ -817,8 +834,6 @@ def prove(cfgs, trace_rows: List[List[int]], pub: List[int], pp: Poseidon2Params
     log["zeta"] = zeta
 
     # ---- TwoAdicFriPcs::open
-    alpha_fri = ch.sample()
-    log["alpha_fri"] = alpha_fri
     N = h << lb
     logN = log_h + lb
     invd = dict(zip((zeta, zeta_next), inverse_denominators(logN, GENERATOR, [zeta, zeta_next])))
@@ -828,6 +843,10 @@ def prove(cfgs, trace_rows: List[List[int]], pub: List[int], pp: Poseidon2Params
     ys_next = interpolate_coset(low, GENERATOR, zeta_next)
     qlow = q_lde[:h]
     ys_q = interpolate_coset(qlow, GENERATOR, zeta)   # one value per chunk (width-1 matrices)
+    if fri.observe_opened_values:  # U7: (matrix, point) order
+        ch.observe_slice(ys_zeta + ys_next + ys_q)
+    alpha_fri = ch.sample()
+    log["alpha_fri"] = alpha_fri
 
     ro = [0] * N
     off = 1  # alpha_fri^num_reduced
@@ -852,7 +871,8 @@ def prove(cfgs, trace_rows: List[List[int]], pub: List[int], pp: Poseidon2Params
     coeffs = idft(fin)
     final_poly = coeffs[0]
     assert all(c == 0 for c in coeffs[1 << fri.log_final_poly_len:]), "final poly degree too high"
-    ch.observe(final_poly)
+    if fri.observe_final_poly:
+        ch.observe(final_poly)
     log["betas"] = betas
     pow_w = ch.grind(fri.proof_of_work_bits)
 
@@ -883,15 +903,19 @@ def verify(cfgs, proof: Proof, pub: List[int], pp: Poseidon2Params, fri: FriPara
     q = 1 << log_q
     lb = fri.log_blowup
     logN = log_h + lb
-    ch = HashChallenger(pp)
-    ch.observe(log_h)
+    ch = HashChallenger(pp, mont_bits=fri.sample_bits_montgomery)
+    if fri.observe_log_degree:
+        ch.observe(log_h)
     ch.observe(proof.trace_root)
-    ch.observe_slice(pub)
+    if fri.observe_public_values:
+        ch.observe_slice(pub)
     alpha = ch.sample()
     ch.observe(proof.quotient_root)
     zeta = ch.sample()
     wh = two_adic_generator(log_h)
     zeta_next = zeta * wh % P
+    if fri.observe_opened_values:
+        ch.observe_slice(list(proof.trace_local) + list(proof.trace_next) + list(proof.quotient_chunks))
     alpha_fri = ch.sample()
     betas = []
     for root in proof.fri_roots:
@@ -899,7 +923,8 @@ def verify(cfgs, proof: Proof, pub: List[int], pp: Poseidon2Params, fri: FriPara
         betas.append(ch.sample())
     if len(proof.fri_roots) != logN - lb - fri.log_final_poly_len:
         return False
-    ch.observe(proof.final_poly)
+    if fri.observe_final_poly:
+        ch.observe(proof.final_poly)
     if not ch.check_witness(fri.proof_of_work_bits, proof.pow_witness):
         return False
     gN = two_adic_generator(logN)

@@ -75,6 +75,18 @@ pub struct Params {
     pub num_queries: u32,
     pub proof_of_work_bits: u32,
     pub public_degree: i32,
+    /// U7: `challenger.observe(log_degree)` before the trace root (default true)
+    pub observe_log_degree: bool,
+    /// U7: `challenger.observe_slice(public_values)` before alpha (default true)
+    pub observe_public_values: bool,
+    /// U7: `TwoAdicFriPcs::open` observes the opened values before alpha_fri
+    /// (default false; later upstream Plonky3 does)
+    pub observe_opened_values: bool,
+    /// U8: `sample_bits` from the Montgomery form's low bits (default false:
+    /// the canonical value's)
+    pub sample_bits_montgomery: bool,
+    /// U12: the final polynomial is observed before grinding (default true)
+    pub observe_final_poly: bool,
     /// U2: the internal layer's diagonal d (s_i <- sum + d_i s_i); None =
     /// (1, 1, 2).  Must be the diagonal of the fork's
     /// `Poseidon2InternalLayerBls12337<3>`, which [`perm`] instantiates.
@@ -158,6 +170,11 @@ impl Default for Params {
             num_queries: 33,
             proof_of_work_bits: 0,
             public_degree: 1,
+            observe_log_degree: true,
+            observe_public_values: true,
+            observe_opened_values: false,
+            sample_bits_montgomery: false,
+            observe_final_poly: true,
             internal_diag: None,
             external_mds: None,
         }
@@ -180,6 +197,7 @@ impl Ctx {
         let rc = p.resolved_round_constants();
         let rc_ptr = fr_ptr(&rc);
         let raw_params = sys::lsp_params {
+            struct_size: std::mem::size_of::<sys::lsp_params>() as u32,
             sbox_degree: p.sbox_degree,
             rounds_f: p.rounds_f,
             rounds_p: p.rounds_p,
@@ -191,6 +209,11 @@ impl Ctx {
             public_degree: p.public_degree,
             internal_diag: p.internal_diag.as_ref().map_or(std::ptr::null(), |d| fr_ptr(d)),
             external_mds: p.external_mds.as_ref().map_or(std::ptr::null(), |m| fr_ptr(m)),
+            skip_log_degree: (!p.observe_log_degree) as u32,
+            skip_public_values: (!p.observe_public_values) as u32,
+            observe_opened_values: p.observe_opened_values as u32,
+            sample_bits_montgomery: p.sample_bits_montgomery as u32,
+            skip_final_poly: (!p.observe_final_poly) as u32,
         };
         let mut out: *mut sys::lsp_ctx = std::ptr::null_mut();
         let rc = unsafe { sys::lsp_ctx_create(device, &raw_params, &mut out) };

@@ -228,3 +228,17 @@ def test_phase_timing_arguments(host_ctx, product_lib):
     assert product_lib.lsp_ctx_set_phase_timing(host_ctx.h, 1, names, 1) == _lib.LSP_OK
     host_ctx.set_phase_timing(False)
     host_ctx.set_phase_timing(True)
+
+
+@pytest.mark.parametrize("logn,ncols,log_q,fri", [(3, 3, 2, {}), (6, 6, 3, {}), (5, 3, 2, dict(num_queries=7)),
+                                                   (6, 3, 2, dict(log_blowup=4, log_final_poly_len=2))])
+def test_wire_size_formula_matches_oracle_proofs(oracle_lib, logn, ncols, log_q, fri):
+    """proof.wire_size (what the 2^26 rank rehearsal's proof size is checked
+    against, tests/test_gpu_configs_full.py) against real serialized proofs"""
+    from linea_stark_prover_amd.proof import wire_size
+    from oracle import pyoracle as O
+    p = oracle_lib.setup()
+    tb, w = oracle_lib.gen_perm_trace(p, logn, ncols)
+    fp = O.FriParams(**fri)
+    proof = oracle_lib.prove(p, tb, 1 << logn, w, oracle_lib.perm_air(ncols), fri=oracle_lib.fri_params(fp))
+    assert len(proof) == wire_size(logn, w, log_q, fp.log_blowup, fp.log_final_poly_len, fp.num_queries)

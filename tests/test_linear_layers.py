@@ -122,7 +122,9 @@ def test_bad_layer_values_rejected(product_lib):
     rc = _rc(s)
     diag = to_mont(DIAG)
     diag[1] = np.array([~np.uint64(0)] * 4, np.uint64)  # not canonical
-    p = _lib.LspParams(11, 8, 22, rc.ctypes.data, 3, 0, 33, 0, 1, diag.ctypes.data, None)
+    p = _lib.LspParams(sbox_degree=11, rounds_f=8, rounds_p=22, round_constants=rc.ctypes.data, log_blowup=3,
+                       log_final_poly_len=0, num_queries=33, proof_of_work_bits=0, public_degree=1,
+                       internal_diag=diag.ctypes.data, external_mds=None)
     h = ctypes.c_void_p()
     assert product_lib.lsp_ctx_create(-1, ctypes.byref(p), ctypes.byref(h)) == _lib.LSP_E_ARG
 

@@ -45,9 +45,10 @@ class Side:
         a, d, rc = cfg.seeded()
         self.rc = rc
         self.pub = np.ascontiguousarray(np.concatenate([a, d]))
-        p = _lib.LspParams(cfg.sbox_degree, cfg.rounds_f, cfg.rounds_p, rc.ctypes.data, cfg.log_blowup,
-                           cfg.log_final_poly_len, cfg.num_queries, cfg.proof_of_work_bits, cfg.public_degree,
-                           None, None)
+        p = _lib.LspParams(sbox_degree=cfg.sbox_degree, rounds_f=cfg.rounds_f, rounds_p=cfg.rounds_p,
+                           round_constants=rc.ctypes.data, log_blowup=cfg.log_blowup,
+                           log_final_poly_len=cfg.log_final_poly_len, num_queries=cfg.num_queries,
+                           proof_of_work_bits=cfg.proof_of_work_bits, public_degree=cfg.public_degree)
         self.h = ctypes.c_void_p()
         self._chk(L.lsp_ctx_create(0, ctypes.byref(p), ctypes.byref(self.h)))
         self.rows, self.w = 1 << log_n, 2 * ncols + 2

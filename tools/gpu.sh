@@ -1,0 +1,81 @@
+#!/bin/bash
+# The one GPU-box driver script (replaces round 3's single-use gpu_r03*.sh):
+#
+#   bash tools/gpu.sh TAG STEP [STEP ...]
+#
+# Steps run in order; each GPU step has its own time limit and the script
+# stops at the first failure (nothing more touches the GPU after a fault,
+# abort or timeout).  Logs and results go to gpurun_out/<step>_<TAG>.*.
+#
+#   tests            every GPU test (pytest -m gpu)
+#   tests:<files>    the listed test files only, comma-separated (tests/ implied)
+#   smoke            __graft_entry__.smoke()
+#   bench            the default bench line (what the driver runs)
+#   benchq           a quick bench: main leg only, no CPU baseline / extra legs
+#   prof             rocprofv3 kernel trace (+ --stats) of a quick bench
+#   pmc              the PMC passes bench.py's roofline reads (tools/pmc_stamp.sh)
+#   rehearse         ranks 0, 5, 7 of the 2^26 proof over 8 ranks (tools/rank_rehearsal.py)
+#   py:<script>      python <script> under a 300 s limit (tools/ implied), output to a log
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${1:?usage: tools/gpu.sh TAG STEP...}
+shift
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+
+fail() { echo "FAILED: $1"; tail -40 "$2"; exit 1; }
+
+for step in "$@"; do
+  echo "=== $step ($(date +%T))"
+  case "$step" in
+    tests)
+      log=gpurun_out/tests_$TAG.log
+      timeout -k 10 1000 $PYT -m gpu tests > $log 2>&1 || fail "$step" $log
+      tail -2 $log ;;
+    tests:*)
+      log=gpurun_out/tests_$TAG.log
+      files=$(echo "${step#tests:}" | tr ',' '\n' | sed 's#^#tests/#' | tr '\n' ' ')
+      timeout -k 10 1000 $PYT -v $files >> $log 2>&1 || fail "$step" $log
+      grep -E "passed|failed" $log | tail -1 ;;
+    smoke)
+      log=gpurun_out/smoke_$TAG.log
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $log 2>&1 || fail "$step" $log
+      cat $log ;;
+    bench)
+      timeout -k 10 900 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
+        || fail "$step" gpurun_out/bench_$TAG.err
+      cut -c1-600 gpurun_out/bench_$TAG.json ;;
+    benchq)
+      timeout -k 10 400 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --inflight 0 --shard-leg none \
+        --batch-leg none --shape-leg none --no-host-trace-leg > gpurun_out/benchq_$TAG.json \
+        2> gpurun_out/benchq_$TAG.err || fail "$step" gpurun_out/benchq_$TAG.err
+      python -c "import json; d=json.load(open('gpurun_out/benchq_$TAG.json')); print(d['ms_per_step'], d['prove_time_median_s'], d['roofline']['ms'], d['roofline_valu']['ms'])" ;;
+    prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o bench -- \
+        python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --inflight 0 --shard-leg none --batch-leg none \
+        --shape-leg none --no-host-trace-leg > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.err \
+        || fail "$step" gpurun_out/prof_$TAG.err
+      echo "kernel trace in gpurun_out/prof_$TAG" ;;
+    pmc)
+      bash tools/pmc_stamp.sh pmc_$TAG || exit 1 ;;
+    rehearse)
+      log=gpurun_out/rehearse_$TAG.jsonl
+      for r in 0 5 7; do
+        timeout -k 10 400 python tools/rank_rehearsal.py --log-n 26 --size 8 --ranks $r --steps 2 >> $log \
+          2>> gpurun_out/rehearse_$TAG.err || fail "$step" gpurun_out/rehearse_$TAG.err
+      done
+      python -c "
+import json
+for l in open('$log'):
+    if l.startswith('{'):
+        d = json.loads(l); print(d['rank'], round(d['prove_s_median'], 4), d['device_used_gib'], d['proof_wire_bytes'])" ;;
+    py:*)
+      script=${step#py:}
+      log=gpurun_out/$(basename ${script%% *} .py)_$TAG.log
+      timeout -k 10 300 python tools/$script > $log 2>&1 || fail "$step" $log
+      tail -20 $log ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "=== done ($(date +%T))"

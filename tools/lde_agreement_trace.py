@@ -1,5 +1,5 @@
 """The bench's event-timed trace LDE (roofline.ms, the last timed step) against
-the rocprofv3 kernel trace of the same command (tools/gpu_round.sh 'rocprof'
+the rocprofv3 kernel trace of the same command (tools/gpu.sh 'rocprof'
 step): per proof, the trace LDE is the first three k_ntt_rm dispatches (inverse
 pass, fused pass, in-place pass; the quotient LDE's three follow).
 

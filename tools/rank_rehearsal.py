@@ -7,10 +7,13 @@ BASELINE configs[3] (the 3x3 permutation AIR at 2^26 rows over 8 MI355X) needs
 (a fresh device and pool): it proves the full-size trace as rank g of G with
 the loopback transport (lsp_ctx_attach_loopback: peers' parts of each exchange
 fabricated locally), so its device memory and per-phase times are rank g's
-at the real shapes.  The proof is not valid and is not checked.  Prints one
+at the real shapes.  The proof is not valid (the library refuses to serialize
+it; only its wire size is read, which must be the real proof's).  Prints one
 JSON object per rank: wall time per step, the phase times of the last step,
-the context's pool (the high-water mark of its working set) and the GPU's
-used memory, against its total.
+the context's pool (the high-water mark of its working set), the GPU's used
+memory against its total, the proof's wire size and the collective schedule
+the rank issued (lsp_comm_log: op, bytes, root, what it carried, device ms).
+tests/test_gpu_configs_full.py runs it at BASELINE configs[3]'s size.
 """
 import argparse
 import json
@@ -50,22 +53,29 @@ def one_rank(log_n, rank, size, steps, ncols=3):
     dtrace = ctx.gen_permutation_trace_device(log_n, ncols, a, d)
     ctx.synchronize()
     gen_s = time.perf_counter() - t
-    S.prove_sharded(ctx, dtrace, air, pub, h, w)  # warm-up: pool, tables
+    nbytes = S.prove_sharded(ctx, dtrace, air, pub, h, w, size_only=True)  # warm-up: pool, tables
     ts = []
     for _ in range(steps):
         ctx.synchronize()
         t = time.perf_counter()
-        S.prove_sharded(ctx, dtrace, air, pub, h, w)
+        nbytes = S.prove_sharded(ctx, dtrace, air, pub, h, w, size_only=True)
         ctx.synchronize()
         ts.append(time.perf_counter() - t)
     phases = {k: round(v, 3) for k, v in ctx.last_timings()}
+    sched, _ = ctx.comm_log()
+    try:  # a rehearsal proof is refused as bytes: the library marks it
+        S.prove_sharded(ctx, dtrace, air, pub, h, w)
+        refused = False
+    except L.LspError as e:
+        refused = e.code == L.LSP_E_STATE
     pool, used, tot = mem()
     trace_bytes = h * w * 32
     return {"log_n": log_n, "rank": rank, "size": size, "steps": steps, "step_s": [round(x, 4) for x in ts],
             "prove_s_median": sorted(ts)[len(ts) // 2], "trace_gen_s": round(gen_s, 3), "phases_ms": phases,
             "trace_bytes": trace_bytes, "pool_bytes": pool, "device_used_bytes": used, "device_total_bytes": tot,
             "pool_plus_trace_gib": round((pool + trace_bytes) / 2**30, 2), "device_used_gib": round(used / 2**30, 2),
-            "fits_288gb": used < 288e9}
+            "fits_288gb": used < 288e9, "proof_wire_bytes": nbytes, "rehearsal_bytes_refused": refused,
+            "comm_log": sched}
 
 
 def main():

@@ -79,7 +79,15 @@ int main(int argc, char** argv) {
     std::vector<lsp_fr> rc(3 * 8 + 22);
     lsp_fr alpha, delta;
     if (lsp_seeded_setup(0x4C494E4541ull, 8, 22, &alpha, &delta, rc.data()) != LSP_OK) return 3;
-    lsp_params prm = {11, 8, 22, rc.data(), 3, 0, 33, 0, 1};
+    lsp_params prm{};
+    prm.struct_size = sizeof prm;
+    prm.sbox_degree = 11;
+    prm.rounds_f = 8;
+    prm.rounds_p = 22;
+    prm.round_constants = rc.data();
+    prm.log_blowup = 3;
+    prm.num_queries = 33;
+    prm.public_degree = 1;
     const char* nq = std::getenv("LSP_SAN_QUERIES");
     if (nq) prm.num_queries = (uint32_t)std::atoi(nq);
     lsp_ctx* ctx = nullptr;

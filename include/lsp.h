@@ -122,7 +122,17 @@ typedef struct {
 } lsp_params;
 
 /* ---------------------------------------------------------------- library */
+/* "... (gfx950)", or "... (gfx950, debug-bounds)" for the bounds-checked
+ * debug build (python -m linea_stark_prover_amd.build --debug-bounds ->
+ * liblsp_hip_dbg.so): every kernel checks its geometry-derived
+ * indices, a failed check skips the access (no fault) and fails the C-ABI
+ * call that launched it with LSP_E_STATE "device bounds check failed at
+ * <file>:<line>". */
 const char *lsp_version(void);
+/* the debug build's self-test: one deliberately failing check on the device,
+ * so LSP_E_STATE with that message; the product build answers LSP_E_STATE
+ * "not a debug-bounds build" */
+int lsp_debug_bounds_probe(lsp_ctx *ctx);
 int lsp_device_count(int *n);
 const char *lsp_last_error(const lsp_ctx *ctx);
 

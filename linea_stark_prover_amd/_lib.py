@@ -58,6 +58,7 @@ class LspError(RuntimeError):
 # name -> (restype, argtypes)
 _SIGS = {
     "lsp_version": (ctypes.c_char_p, []),
+    "lsp_debug_bounds_probe": (ctypes.c_int, [ctypes.c_void_p]),
     "lsp_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "lsp_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "lsp_seeded_setup": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, c_fr_p, c_fr_p, c_fr_p]),

@@ -1,11 +1,15 @@
 """Build liblsp_hip.so (HIP kernels + host orchestration) for gfx950, in-tree.
 
-    python -m linea_stark_prover_amd.build [--force] [-j N]
+    python -m linea_stark_prover_amd.build [--force] [-j N] [--debug-bounds]
 
 Objects go to ``linea_stark_prover_amd/_build/``, the library to
 ``linea_stark_prover_amd/_lib/liblsp_hip.so`` (git-ignored, travels to the GPU
 box with the snapshot).  Rebuilds only what changed (any header change
 rebuilds everything).
+
+``--debug-bounds``: the bounds-checked debug build (csrc/dbg_bounds.hpp)
+-- ``-DLSP_DEBUG_BOUNDS``, objects in ``_build_dbg/``, library
+``_lib/liblsp_hip_dbg.so``; select it with ``LSP_LIB=<path>`` (linea_stark_prover_amd/_lib.py).
 """
 from __future__ import annotations
 
@@ -76,53 +80,62 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src):
-    obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
-    cmd = [HIPCC] + CFLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
+DBG_BUILD = os.path.join(PKG, "_build_dbg")
+DBG_LIB = os.path.join(LIBDIR, "liblsp_hip_dbg.so")
+
+
+def _compile(src, build_dir=BUILD, extra=()):
+    obj = os.path.join(build_dir, os.path.splitext(src)[0] + ".o")
+    flags = CFLAGS + list(extra)
+    cmd = [HIPCC] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
     if src.endswith(".cpp"):
-        cmd = [HIPCC] + CFLAGS + ["-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [HIPCC] + flags + ["-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     return obj
 
 
-def build(force: bool = False, jobs: int = None, verbose: bool = True) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(force: bool = False, jobs: int = None, verbose: bool = True, debug_bounds: bool = False) -> str:
+    build_dir, lib = (DBG_BUILD, DBG_LIB) if debug_bounds else (BUILD, LIB)
+    extra = ["-DLSP_DEBUG_BOUNDS"] if debug_bounds else []
+    os.makedirs(build_dir, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     hdrs = _headers()
     todo = []
     objs = []
     for s in SOURCES:
-        obj = os.path.join(BUILD, os.path.splitext(s)[0] + ".o")
+        obj = os.path.join(build_dir, os.path.splitext(s)[0] + ".o")
         objs.append(obj)
         if force or _stale(obj, [os.path.join(CSRC, s)] + hdrs):
             todo.append(s)
     jobs = jobs or min(len(todo) or 1, os.cpu_count() or 4, 16)
     if todo:
         if verbose:
-            print(f"[lsp build] compiling {len(todo)} file(s) for {ARCH}: {' '.join(todo)}", flush=True)
+            print(f"[lsp build] compiling {len(todo)} file(s) for {ARCH}{' (debug-bounds)' if debug_bounds else ''}: "
+                  f"{' '.join(todo)}", flush=True)
         with cf.ThreadPoolExecutor(jobs) as ex:
-            list(ex.map(_compile, todo))
-    if todo or _stale(LIB, objs):
-        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs + ["-lpthread", "-ldl"]
+            list(ex.map(lambda src: _compile(src, build_dir, extra), todo))
+    if todo or _stale(lib, objs):
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", lib] + objs + ["-lpthread", "-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         if verbose:
-            print(f"[lsp build] linked {LIB}", flush=True)
-    if library_hash() != source_hash():
+            print(f"[lsp build] linked {lib}", flush=True)
+    if not debug_bounds and library_hash() != source_hash():
         with open(STAMP, "w") as fh:
             fh.write(source_hash() + "\n")
-    return LIB
+    return lib
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=None)
+    ap.add_argument("--debug-bounds", action="store_true", help="the bounds-checked debug library (liblsp_hip_dbg.so)")
     a = ap.parse_args(argv)
-    build(a.force, a.j)
+    build(a.force, a.j, debug_bounds=a.debug_bounds)
 
 
 if __name__ == "__main__":

@@ -14,10 +14,41 @@ using namespace lsp;
 namespace {
 thread_local std::string g_err;  // errors without a context
 
+#ifdef LSP_DEBUG_BOUNDS
+// The debug build: every kernel translation unit's fault word after a C-ABI
+// call (dbg_bounds.hpp), with its (file code, line) mapped back to a name
+std::string bounds_fault_report() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return "";
+    (void)hipDeviceSynchronize();  // the call's kernels are done (any stream)
+    static const char* const files[] = {"k_ntt.hip", "k_hash.hip", "k_field.hip", "k_quotient.hip", "k_open.hip",
+                                        "k_witness.hip", "fr29.hpp", "k_common.hpp", "poseidon2_f29.hpp", "fr.hpp"};
+    static unsigned (*const readers[])() = {bounds_fault_k_ntt, bounds_fault_k_hash, bounds_fault_k_field,
+                                            bounds_fault_k_quotient, bounds_fault_k_open, bounds_fault_k_witness};
+    static const char* const tus[] = {"k_ntt.hip", "k_hash.hip", "k_field.hip", "k_quotient.hip", "k_open.hip",
+                                      "k_witness.hip"};
+    std::string out;
+    for (size_t t = 0; t < sizeof readers / sizeof readers[0]; ++t) {
+        const unsigned v = readers[t]();
+        if (!v) continue;
+        std::string file = "file#" + std::to_string(v >> 16);
+        for (const char* f : files)
+            if (dbg::file_code(f) == (v >> 16)) file = f;
+        out += (out.empty() ? "" : "; ") + std::string("device bounds check failed at ") + file + ":" +
+               std::to_string(v & 0xffffu) + " (kernels of " + tus[t] + ")";
+    }
+    return out;
+}
+#endif
+
 template <class F>
 int guarded(lsp_ctx* ctx, F&& f) {
     try {
         f();
+#ifdef LSP_DEBUG_BOUNDS
+        const std::string bad = bounds_fault_report();
+        if (!bad.empty()) throw LspError(LSP_E_STATE, bad);
+#endif
         return LSP_OK;
     } catch (const LspError& e) {
         (ctx ? ctx->err : g_err) = e.what();
@@ -91,7 +122,26 @@ struct SplitMix64 {
 
 extern "C" {
 
+#ifdef LSP_DEBUG_BOUNDS
+const char* lsp_version(void) { return "linea_stark_prover_amd 0.1 (gfx950, debug-bounds)"; }
+#else
 const char* lsp_version(void) { return "linea_stark_prover_amd 0.1 (gfx950)"; }
+#endif
+
+int lsp_debug_bounds_probe(lsp_ctx* ctx) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx, LSP_E_ARG, "null ctx");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+#ifndef LSP_DEBUG_BOUNDS
+        throw LspError(LSP_E_STATE, "not a debug-bounds build (python -m linea_stark_prover_amd.build --debug-bounds)");
+#else
+        uint32_t* sink = (uint32_t*)ctx->buf("bounds_probe", 4 * sizeof(uint32_t));
+        LSP_HIP(launch_bounds_probe(sink, ctx->stream));
+        ctx->sync();  // guarded() then reports the probe's failed check as LSP_E_STATE
+#endif
+    });
+}
 
 int lsp_device_count(int* n) {
     return guarded(nullptr, [&] {
@@ -204,6 +254,9 @@ int lsp_ctx_create(int device, const lsp_params* p, lsp_ctx** out) {
             LSP_REQUIRE(device >= 0 && device < n, LSP_E_ARG, "bad device index");
             LSP_HIP(hipSetDevice(device));
             LSP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            int lds = 0;  // LDS per workgroup (gfx950: 160 KiB): what the reduce-rows launch may use
+            if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lds > 0)
+                c->lds_per_block = (size_t)lds;
             LSP_HIP(hipMalloc(&c->rc_dev, nrc * sizeof(Fr)));
             LSP_HIP(hipMemcpy(c->rc_dev, c->p2.rc.data(), nrc * sizeof(Fr), hipMemcpyHostToDevice));
             LSP_HIP(hipMalloc(&c->rc29_dev, nrc * sizeof(F29)));
@@ -582,6 +635,7 @@ int lsp_quotient_values(lsp_ctx* ctx, const lsp_fr* lde, size_t h, size_t w, con
         qa.inv_zh = dz + q;
         qa.inv_den = inv_den;
         qa.out = dout;
+        qa.lde_rows = (uint64_t)h << ctx->log_blowup;
         LSP_HIP(launch_quotient(qa, ctx->stream));
         finish_out(ctx, out, dout, Q, mem);
     });

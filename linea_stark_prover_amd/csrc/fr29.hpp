@@ -15,6 +15,7 @@
 // from: repack bits, Montgomery-multiply by 2^266 mod r (x 2^5);
 // to:   Montgomery-multiply by 2^256 mod r (x 2^-5), reduce to [0, r), repack.
 #pragma once
+#include "dbg_bounds.hpp"
 #include "fr.hpp"
 
 namespace lsp {
@@ -219,7 +220,9 @@ __device__ __forceinline__ void f29_qtab_init(uint4* t) {
 }
 
 __device__ __forceinline__ F29 f29_reduce_qt(const F29& a, const uint4* __restrict__ t) {
-    const uint32_t q = __umulhi(a.l[8], 0xdb651d12u) >> 20;  // as f29_reduce
+    uint32_t q = __umulhi(a.l[8], 0xdb651d12u) >> 20;  // as f29_reduce
+    // a value outside the documented bounds (top limb too large) would index past the table
+    if (!LSP_BOUNDS(q < F29_QTAB_N)) q = 0;
     const uint4 x = t[3 * q], y = t[3 * q + 1];
     const uint32_t z = reinterpret_cast<const uint32_t*>(t + 3 * q + 2)[0];
     const uint32_t T[9] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z};

@@ -277,6 +277,7 @@ struct lsp_ctx {
     lsp::Fr* rc_dev = nullptr;    // round constants, ark form
     lsp::F29* rc29_dev = nullptr; // the same in the 29-bit-limb form the hash kernels use
     uint32_t log_blowup = 3, log_final_poly_len = 0, num_queries = 33, pow_bits = 0;
+    size_t lds_per_block = 64 * 1024;  // the device's LDS per workgroup (hipDeviceAttributeMaxSharedMemoryPerBlock)
     int32_t public_degree = 1;
     lsp::TranscriptCfg transcript;  // U7/U8/U12 (lsp_params)
     std::string err;

@@ -196,7 +196,18 @@ __global__ __launch_bounds__(256) void k_assemble_chunks(const Fr* __restrict__ 
     if (i >= (Sq << logGq)) return;
     out[i] = stage[brev_bits(i & ((1ull << logGq) - 1), logGq) * Sq + (i >> logGq)];
 }
+// the debug build's self-test (lsp_debug_bounds_probe): one check that must
+// fail, on an index one past its extent; nothing is accessed
+__global__ void k_bounds_probe(uint32_t n, uint32_t* __restrict__ sink) {
+    const uint32_t i = n + threadIdx.x;  // == n for the one thread
+    if (LSP_BOUNDS(i < n)) sink[i] = 1u;
+}
 }  // namespace
+
+hipError_t launch_bounds_probe(uint32_t* sink, hipStream_t st) {
+    hipLaunchKernelGGL(k_bounds_probe, dim3(1), dim3(1), 0, st, 1u, sink);
+    return hipGetLastError();
+}
 
 size_t batch_inverse_scratch(size_t n) {
     size_t tot = 0;
@@ -252,3 +263,5 @@ hipError_t launch_assemble_chunks(const Fr* stage, uint32_t logGq, size_t Sq, Fr
 }
 
 }  // namespace lsp
+
+LSP_BOUNDS_READER(k_field)

@@ -51,7 +51,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSP_P2_ROWS
     const size_t i = gtid() / LANES;
     if (i >= nrows) return;
     const Fr* row = m + i * w;
-    const Fr d = sponge_f29<D, LANES>([&](uint32_t k) { return row[k]; }, w, rc, rf, rp, qt);
+    const Fr d = sponge_f29<D, LANES>([&](uint32_t k) { return LSP_BOUNDS(k < w) ? row[k] : fr_zero(); }, w, rc, rf,
+                                      rp, qt);
     if ((threadIdx.x & (LANES - 1)) == 0) out[i] = d;
 }
 
@@ -70,6 +71,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSP_P2_ROWS
         while (k >= ml.width[j]) {
             k -= ml.width[j];
             ++j;
+            if (!LSP_BOUNDS(j < ml.n)) return fr_zero();
         }
         return ml.ptr[j][i * ml.width[j] + k];
     };
@@ -108,6 +110,7 @@ __global__ __launch_bounds__(256) void k_merkle_level(const Fr* __restrict__ src
     __syncthreads();
     const size_t i = gtid() / LANES;
     if (i >= nout) return;
+    if (!LSP_BOUNDS(2 * i + 1 < 2 * nout)) return;
     const Fr d = compress_f29<D, LANES>(src[2 * i], src[2 * i + 1], rc, rf, rp, qt);
     if ((threadIdx.x & (LANES - 1)) == 0) dst[i] = d;
 }
@@ -122,6 +125,7 @@ __global__ __launch_bounds__(256) void k_merkle_top(Fr* __restrict__ layers, siz
     f29_qtab_init(qt);
     __syncthreads();
     __shared__ Fr buf[128];
+    if (!LSP_BOUNDS(len <= 128)) return;
     for (uint32_t e = threadIdx.x; e < len; e += blockDim.x) buf[e] = layers[off + e];
     __syncthreads();
     size_t out_off = off + len;
@@ -364,3 +368,5 @@ hipError_t launch_merkle_tree(Fr* layers, size_t nleaves, const F29* rc, P2Layou
 }
 
 }  // namespace lsp
+
+LSP_BOUNDS_READER(k_hash)

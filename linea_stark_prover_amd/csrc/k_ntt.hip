@@ -241,6 +241,7 @@ __device__ __forceinline__ void dit4(F29& v0, F29& v1, F29& v2, F29& v3, const F
 // 2^(logH - k)): the coefficients never go to HBM.
 constexpr uint32_t NTT_THREADS = 256;
 constexpr uint32_t NTT_MAX_EL = 1024;  // 2^k x G x CW
+__device__ __forceinline__ uint32_t k_pos(uint32_t k) { return 1u << k; }  // positions of a tile
 
 template <int LOGCW>
 struct TileGeom {
@@ -286,7 +287,8 @@ __device__ __forceinline__ uint32_t twl_index(const TileGeom<LOGCW>& gm, uint32_
 template <bool DIF, int LOGCW>
 __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOGCW>& gm, const uint4* __restrict__ tw,
                                             uint32_t s0, uint32_t logH, uint32_t n_el,
-                                            const uint4* twl = nullptr, const uint4* qt = nullptr) {
+                                            const uint4* twl = nullptr, const uint4* qt = nullptr,
+                                            uint32_t twl_n = 0) {
     constexpr uint32_t CW = 1u << LOGCW;
     const uint32_t k = gm.k, G = 1u << gm.logG;
     const uint32_t cshift = gm.logG + LOGCW;  // element index = (t << cshift) + (g << LOGCW) + c
@@ -296,8 +298,12 @@ __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOG
         // DIF w^((row mod H/2^(s+1)) 2^s), DIT w^((row mod 2^s) 2^(logH-1-s)); the
         // table is stage-major (entry 2^(m-1) - 1 + i = w_(2^m)^i), so
         // consecutive rows read consecutive slots
-        if (DIF && twl) return f29_load48(twl + 3 * twl_index(gm, row, s));  // the fused pass's LDS copy
+        if (DIF && twl) {  // the fused pass's LDS copy
+            const uint32_t ti = twl_index(gm, row, s);
+            return f29_load48(twl + 3 * (LSP_BOUNDS(ti < twl_n) ? ti : 0u));
+        }
         const uint32_t half = DIF ? (uint32_t)(H >> (s + 1)) : (1u << s);
+        if (!LSP_BOUNDS(s < logH && row < H)) return f29_zero();
         return f29_load48(tw + 3 * (size_t)(half - 1 + (row & (half - 1))));
     };
     uint32_t j = 0;
@@ -317,6 +323,7 @@ __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOG
                 const uint32_t g = pg & (G - 1), pp = pg >> gm.logG;
                 const uint32_t t0 = ((pp & ~bmask) << 2) | (pp & bmask);
                 const uint32_t e0 = (t0 << cshift) + (g << LOGCW) + c, de = (1u << b) << cshift;
+                if (!LSP_BOUNDS(e0 + 3 * de < n_el && t0 + 3 * (1u << b) < k_pos(k))) continue;
                 F29 v0 = T.get(e0), v1 = T.get(e0 + de), v2 = T.get(e0 + 2 * de), v3 = T.get(e0 + 3 * de);
                 const uint32_t r0 = gm.row_of(t0, g), dr = (1u << b) << gm.logL;
                 if constexpr (DIF) {
@@ -353,6 +360,7 @@ __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOG
             const uint32_t g = pg & (G - 1), pp = pg >> gm.logG;
             const uint32_t t0 = ((pp >> logd) << (logd + 1)) | (pp & dmask);
             const uint32_t a0 = (t0 << cshift) + (g << LOGCW) + c, a1 = a0 + ((1u << logd) << cshift);
+            if (!LSP_BOUNDS(a1 < n_el)) continue;
             const F29 a = T.get(a0), b = T.get(a1);
             if (trivial) {
                 T.put(a0, red(f29_lazy2(a, b), qt));
@@ -429,6 +437,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
             const uint32_t u = r - (K - (K >> sk));
             const uint32_t half = (uint32_t)(H >> (sk + 1));
             const size_t gi = (size_t)(half - 1) + gm.gid0 + g + ((size_t)u << p.logL);
+            if (!LSP_BOUNDS(gi + 1 < H && sk < p.k)) continue;
             twl[3 * e] = p.tw[3 * gi];
             twl[3 * e + 1] = p.tw[3 * gi + 1];
             twl[3 * e + 2] = p.tw[3 * gi + 2];
@@ -445,6 +454,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
             const uint32_t row = gm.row_of(t, g);
             const uint32_t srow = p.inv_gather ? brev_bits(row, p.logH) : row;
             size_t si;
+            if (!LSP_BOUNDS(row < H && gm.idx(t, g, c) < n_el && c0 + c < p.w)) continue;
             T.put(gm.idx(t, g, c), src_at(p.src_map, H, srow, c0 + c, si) ? f29_repack_in(p.src[si]) : f29_zero());
         }
         __syncthreads();
@@ -467,6 +477,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
     const bool chain = FWD_FIRST && p.ratio != nullptr;
     for (uint32_t j = arr0; j < arr_end; ++j) {
         const uint32_t arr = chain ? (uint32_t)brev_bits(j, p.log_narr) : j;
+        if (!LSP_BOUNDS(arr < p.narr)) return;
         Fr* base = p.dst + (size_t)arr * H * p.w;
         if (FWD_FIRST) __syncthreads();  // the previous reads of the tile (and of fac) are done
         // ---- row factors (29-bit form): s^row / h once per row when every column
@@ -476,6 +487,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
             for (uint32_t rg = threadIdx.x; rg < (K << logG); rg += NTT_THREADS) {
                 uint32_t t, g, c;
                 gm.split(rg << LOGCW, t, g, c);
+                if (!LSP_BOUNDS(gm.row_of(t, g) < H && (gm.row_of(t, g) >> p.L1) < (1u << p.L2))) continue;
                 fac[(t << logG) + g] = pow2l29(tab, p.L1, gm.row_of(t, g));
             }
             __syncthreads();
@@ -489,6 +501,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
                 gm.split(e, t, g, c);
                 if (e >= n_el || c >= cw) continue;
                 F29 f;
+                if (!LSP_BOUNDS(((t << logG) + g) < (K << logG) && gm.idx(t, g, c) < n_el)) continue;
                 if (row_twist || (chain && j > 0)) {
                     f = fac[(t << logG) + g];
                 } else {
@@ -508,6 +521,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
                 gm.split(e, t, g, c);
                 if (c >= cw) continue;
                 const uint32_t row = gm.row_of(t, g);
+                if (!LSP_BOUNDS(row < H && gm.idx(t, g, c) < n_el && c0 + c < p.w)) continue;
                 F29 v;
                 size_t si;
                 if (MODE == PASS_INV_FIRST)
@@ -518,13 +532,14 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
             }
         }
         __syncthreads();
-        tile_stages<DIF, LOGCW>(T, gm, p.tw, p.s0, p.logH, n_el, twl, qt);
+        tile_stages<DIF, LOGCW>(T, gm, p.tw, p.s0, p.logH, n_el, twl, qt, p.twl_n);
         // ---- store
         const bool canon = p.canon != 0;
         for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
             uint32_t t, g, c;
             gm.split(e, t, g, c);
             if (c >= cw) continue;
+            if (!LSP_BOUNDS(gm.row_of(t, g) < H && gm.idx(t, g, c) < n_el && c0 + c < p.w)) continue;
             base[(size_t)gm.row_of(t, g) * p.w + c0 + c] = f29_store(T.get(gm.idx(t, g, c)), canon);
         }
     }
@@ -837,3 +852,5 @@ hipError_t launch_powers(const Fr* tab, uint32_t L1, size_t n, Fr* out, hipStrea
 }
 
 }  // namespace lsp
+
+LSP_BOUNDS_READER(k_ntt)

@@ -141,6 +141,9 @@ __global__ __launch_bounds__(256) void k_reduce_rows(ReduceArgs a) {
     __syncthreads();
     const size_t i = gtid();
     if (i >= a.n) return;
+    // the constants' LDS copy: the launch sized it for w + 1 + 2q entries after the table
+    if (!LSP_BOUNDS(GLB || 3 * F29_QTAB_N * sizeof(uint4) + (a.w + 1 + 2 * (size_t)a.q) * sizeof(F29) <= a.lds_max))
+        return;
     const Fr* row = a.lde + i * a.w;
     const Fr* qrow = a.qlde + i * a.q;
     // Software-pipelined loads: the next chunk of the row (then of the quotient
@@ -248,7 +251,7 @@ hipError_t launch_reduce_rows(const ReduceArgs& a, hipStream_t st) {
     const size_t qtab = 3 * F29_QTAB_N * sizeof(uint4);
     const size_t nconst = a.w + 1 + 2 * (size_t)a.q;
     const size_t lds = qtab + nconst * sizeof(F29);
-    if (lds <= REDUCE_ROWS_LDS_MAX) {
+    if (lds <= a.lds_max) {
         hipLaunchKernelGGL(k_reduce_rows<false>, dim3(nblocks(a.n, 256)), dim3(256), lds, st, a);
         return hipGetLastError();
     }
@@ -278,3 +281,5 @@ hipError_t launch_fri_fold(const Fr* v, size_t m, Fr half, Fr half_beta, const F
 }
 
 }  // namespace lsp
+
+LSP_BOUNDS_READER(k_open)

@@ -33,12 +33,16 @@ struct Q29 {
     __device__ __forceinline__ F29 mul(const F29& a, const F29& b) const { return f29_mul(a, b); }
 };
 
-__device__ __forceinline__ F29 ld29(const Fr* __restrict__ row, int32_t k) { return f29_from_fr(row[k]); }
+// column k of a row (the descriptor's ids are checked against the width on
+// the host, Air::parse; the debug build checks them again here)
+__device__ __forceinline__ F29 ld29(const Fr* __restrict__ row, int32_t k, uint32_t w) {
+    return LSP_BOUNDS(k >= 0 && (uint32_t)k < w) ? f29_from_fr(row[k]) : f29_zero();
+}
 
 __device__ __forceinline__ F29 horner(const Q29& F, const Fr* __restrict__ row, const int32_t* __restrict__ ids,
-                                      int32_t n, const F29& a) {
+                                      int32_t n, const F29& a, uint32_t w) {
     F29 acc = f29_zero();
-    for (int32_t k = 0; k < n; ++k) acc = F.add(F.mul(acc, a), ld29(row, ids[k]));
+    for (int32_t k = 0; k < n; ++k) acc = F.add(F.mul(acc, a), ld29(row, ids[k], w));
     return acc;
 }
 
@@ -80,9 +84,13 @@ __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
     const F29 first = F.mul(zh, F.mul(xml29, inv_den));              // Z_H / (x - 1)
     const F29 last = F.mul(zh, F.mul(f29_from_fr(xm1), inv_den));  // Z_H / (x - w^-1)
     const F29 trans = xml29;                                         // x - w^-1
-    const Fr* loc = a.lde + (brev_bits(i, a.logQ) - a.row0) * a.w;
-    const Fr* nxt = a.lde_next ? a.lde_next + (brev_bits((i + (1ull << a.log_q)) & (Q - 1), a.logQ) - a.row0_next) * a.w
-                               : a.lde + (brev_bits((i + (1ull << a.log_q)) & (Q - 1), a.logQ) - a.row0) * a.w;
+    const uint64_t lrow = brev_bits(i, a.logQ) - a.row0;
+    const uint64_t nrow = brev_bits((i + (1ull << a.log_q)) & (Q - 1), a.logQ) - (a.lde_next ? a.row0_next : a.row0);
+    // the rows this rank holds (lde_rows = 0: not given, unchecked)
+    if (!LSP_BOUNDS(a.lde_rows == 0 || (lrow < a.lde_rows && nrow < (a.lde_next ? a.lde_next_rows : a.lde_rows))))
+        return;
+    const Fr* loc = a.lde + lrow * a.w;
+    const Fr* nxt = (a.lde_next ? a.lde_next : a.lde) + nrow * a.w;
     const F29 ap = f29_from_fr(a.pub_alpha), dl = f29_from_fr(a.pub_delta), al = f29_from_fr(a.alpha);
     F29 acc = f29_zero();
 #define PUSH(X) acc = F.add(F.mul(acc, al), (X))
@@ -98,13 +106,13 @@ __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
             const int32_t* bid = d + p;
             p += nb;
             const int32_t binv = d[p++], chk = d[p++];
-            const F29 a_l = F.add(horner(F, loc, aid, na, ap), dl);
-            const F29 b_l = F.add(horner(F, loc, bid, nb, ap), dl);
-            const F29 lbinv = ld29(loc, binv), lchk = ld29(loc, chk);
+            const F29 a_l = F.add(horner(F, loc, aid, na, ap, a.w), dl);
+            const F29 b_l = F.add(horner(F, loc, bid, nb, ap, a.w), dl);
+            const F29 lbinv = ld29(loc, binv, a.w), lchk = ld29(loc, chk, a.w);
             PUSH(F.sub(F.mul(b_l, lbinv), one));
             PUSH(F.mul(first, F.sub(lchk, F.mul(a_l, lbinv))));
-            const F29 a_n = F.add(horner(F, nxt, aid, na, ap), dl);
-            PUSH(F.mul(trans, F.sub(ld29(nxt, chk), F.mul(F.mul(lchk, a_n), ld29(nxt, binv)))));
+            const F29 a_n = F.add(horner(F, nxt, aid, na, ap, a.w), dl);
+            PUSH(F.mul(trans, F.sub(ld29(nxt, chk, a.w), F.mul(F.mul(lchk, a_n), ld29(nxt, binv, a.w)))));
             PUSH(F.mul(last, F.sub(lchk, one)));
         } else {  // AirLookupConfig: air/src/lib.rs:57-114
             const int32_t na = d[p++];
@@ -122,21 +130,21 @@ __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
             const int32_t* occ = d + p;
             p += nt;
             const int32_t chk = d[p++];
-            const F29 a_l = F.add(horner(F, loc, aid, na, ap), dl);
-            const F29 lainv = ld29(loc, ainv);
+            const F29 a_l = F.add(horner(F, loc, aid, na, ap, a.w), dl);
+            const F29 lainv = ld29(loc, ainv, a.w);
             PUSH(F.sub(F.mul(a_l, lainv), one));
-            F29 lc = F.mul(ld29(loc, afil), lainv);
-            F29 nc = F.mul(ld29(nxt, afil), ld29(nxt, ainv));
+            F29 lc = F.mul(ld29(loc, afil, a.w), lainv);
+            F29 nc = F.mul(ld29(nxt, afil, a.w), ld29(nxt, ainv, a.w));
             for (int32_t t = 0; t < nt; ++t) {
-                const F29 b_l = F.add(horner(F, loc, bid + t * nbc, nbc, ap), dl);
-                const F29 lbinv = ld29(loc, binv[t]);
+                const F29 b_l = F.add(horner(F, loc, bid + t * nbc, nbc, ap, a.w), dl);
+                const F29 lbinv = ld29(loc, binv[t], a.w);
                 PUSH(F.sub(F.mul(b_l, lbinv), one));
-                lc = F.sub(lc, F.mul(F.mul(ld29(loc, bfil[t]), ld29(loc, occ[t])), lbinv));
-                nc = F.sub(nc, F.mul(F.mul(ld29(nxt, bfil[t]), ld29(nxt, occ[t])), ld29(nxt, binv[t])));
+                lc = F.sub(lc, F.mul(F.mul(ld29(loc, bfil[t], a.w), ld29(loc, occ[t], a.w)), lbinv));
+                nc = F.sub(nc, F.mul(F.mul(ld29(nxt, bfil[t], a.w), ld29(nxt, occ[t], a.w)), ld29(nxt, binv[t], a.w)));
             }
-            const F29 lchk = ld29(loc, chk);
+            const F29 lchk = ld29(loc, chk, a.w);
             PUSH(F.mul(first, F.sub(lchk, lc)));
-            PUSH(F.mul(trans, F.sub(F.sub(ld29(nxt, chk), lchk), nc)));
+            PUSH(F.mul(trans, F.sub(F.sub(ld29(nxt, chk, a.w), lchk), nc)));
             PUSH(F.mul(last, lchk));
         }
     }
@@ -170,3 +178,5 @@ hipError_t launch_quotient(const QuotientArgs& a, hipStream_t st) {
 }
 
 }  // namespace lsp
+
+LSP_BOUNDS_READER(k_quotient)

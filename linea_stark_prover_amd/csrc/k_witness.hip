@@ -201,7 +201,7 @@ __device__ __forceinline__ bool rec_enabled(uint32_t r, size_t n, const Fr* afil
 // table's mask + 1 slots: the table has at least twice as many slots as
 // records (occ_capacity), and a full sweep returns H_EMPTY rather than spin.
 __device__ __forceinline__ uint32_t occ_slot(const Fr* __restrict__ comb, uint32_t r, uint32_t* rep, uint32_t mask,
-                                             bool insert) {
+                                             bool insert, size_t m) {
     const Fr key = comb[r];
     uint32_t h = key_hash(key) & mask;
     for (uint32_t probe = 0; probe <= mask; ++probe) {
@@ -211,6 +211,7 @@ __device__ __forceinline__ uint32_t occ_slot(const Fr* __restrict__ comb, uint32
             cur = atomicCAS(rep + h, H_EMPTY, r);
             if (cur == H_EMPTY) return h;
         }
+        if (!LSP_BOUNDS(cur < m)) return H_EMPTY;  // a slot holds a record index below m
         if (cur == r || fr_eq(comb[cur], key)) return h;
         h = (h + 1) & mask;
     }
@@ -225,7 +226,7 @@ __global__ __launch_bounds__(256) void k_occ_insert(const Fr* __restrict__ comb,
                                                     uint32_t mask) {
     const size_t r = gtid();
     if (r >= m || !rec_enabled((uint32_t)r, n, afil, bfil)) return;
-    const uint32_t h = occ_slot(comb, (uint32_t)r, rep, mask, true);
+    const uint32_t h = occ_slot(comb, (uint32_t)r, rep, mask, true, m);
     if (h == H_EMPTY) return;  // (a full table: excluded by occ_capacity)
     if (r < n) {
         atomicAdd(cnt + h, 1u);
@@ -243,8 +244,9 @@ __global__ __launch_bounds__(256) void k_occ_assign(const Fr* __restrict__ comb,
                                                     uint32_t* __restrict__ occ) {
     const size_t j = gtid();  // B entry t n + i
     if (j >= n * nt || !fr_nonzero(bfil[j])) return;
-    const uint32_t h = occ_slot(comb, (uint32_t)(n + j), rep, mask, false);
+    const uint32_t h = occ_slot(comb, (uint32_t)(n + j), rep, mask, false, n * (nt + 1));
     if (h == H_EMPTY) return;  // (every enabled B entry was inserted by k_occ_insert)
+    if (!LSP_BOUNDS(h <= mask)) return;
     const size_t t = j / n, i = j - t * n;
     if (minb[h] == (unsigned long long)(i * nt + t)) occ[j] = cnt[h];
 }
@@ -407,3 +409,5 @@ hipError_t launch_lookup_terms(const Fr* inv, const uint32_t* occ, const Fr* afi
 }
 
 }  // namespace lsp
+
+LSP_BOUNDS_READER(k_witness)

@@ -205,6 +205,8 @@ struct QuotientArgs {
     // thread order (launch_quotient sets it; LSP_QUOTIENT_ORDER): 1 = LDE row
     // order (a wave reads 64 adjacent rows, the default), 0 = point order
     uint32_t row_order = 0;
+    // rows held at `lde` / `lde_next` (the debug build's bounds checks; 0 = not given)
+    uint64_t lde_rows = 0, lde_next_rows = 0;
 };
 // den[m] = (x_i - 1)(x_i - w_h^-1), x_i = GEN * w_Q^i, i = i0 + (m << log_step), m < n
 hipError_t launch_selector_denoms(const Fr* tabQ, uint32_t L1, Fr gen, Fr wh_inv, size_t n, Fr* den,
@@ -239,16 +241,28 @@ struct ReduceArgs {
     Fr* out;           // N
     size_t n;
     F29* consts29 = nullptr;  // global scratch of reduce_rows_scratch(w, q) F29 (needed only beyond the LDS)
+    size_t lds_max = 64 * 1024;  // the device's LDS per workgroup (lsp_ctx::lds_per_block)
 };
-// the reduce-rows constants stay in the workgroup's LDS up to this many bytes
-// (gfx950: 160 KiB per workgroup), i.e. w + 2q <= ~4,400 columns; wider
-// matrices keep them in global memory (ReduceArgs::consts29)
-constexpr size_t REDUCE_ROWS_LDS_MAX = 160 * 1024;
-inline size_t reduce_rows_scratch(uint32_t w, uint32_t q) {
+// the reduce-rows constants stay in the workgroup's LDS up to the device's
+// LDS per workgroup (lds_max: gfx950 160 KiB, i.e. w + 2q <= ~4,400 columns,
+// read from the device at context creation); wider matrices keep them in
+// global memory (ReduceArgs::consts29)
+inline size_t reduce_rows_scratch(uint32_t w, uint32_t q, size_t lds_max) {
     const size_t lds = 3 * 64 * 16 + (w + 1 + 2 * (size_t)q) * 36;
-    return lds <= REDUCE_ROWS_LDS_MAX ? 0 : w + 1 + 2 * (size_t)q;
+    return lds <= lds_max ? 0 : w + 1 + 2 * (size_t)q;
 }
 hipError_t launch_reduce_rows(const ReduceArgs& a, hipStream_t st);
+// one deliberately failing LSP_BOUNDS check (dbg_bounds.hpp; a no-op kernel in the product build)
+hipError_t launch_bounds_probe(uint32_t* sink, hipStream_t st);
+#ifdef LSP_DEBUG_BOUNDS
+// each kernel translation unit's bounds-fault word ((file code << 16) | line, 0 = none), read and cleared
+unsigned bounds_fault_k_ntt();
+unsigned bounds_fault_k_hash();
+unsigned bounds_fault_k_field();
+unsigned bounds_fault_k_quotient();
+unsigned bounds_fault_k_open();
+unsigned bounds_fault_k_witness();
+#endif
 // one matrix opened at npts points (the generic reduce of TwoAdicFriPcs::open):
 // ro[i] += sum_p (offys[p] - off[p] * sum_c apw[c] M[i][c]) * inv[p*n + i]
 hipError_t launch_reduce_matrix(const Fr* M, size_t n, uint32_t w, const Fr* apw, uint32_t npts, const Fr* inv,

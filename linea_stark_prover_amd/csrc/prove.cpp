@@ -858,6 +858,8 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             qa.n = Sq;
             qa.lde_next = lde_next;
             qa.row0_next = row0_next;
+            qa.lde_rows = S;
+            qa.lde_next_rows = lde_next ? S : 0;
             LSP_HIP(launch_quotient(qa, st));
         }
         if (G > 1) {
@@ -1038,7 +1040,8 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         ra.ryq = dapw + napw;
         ra.out = fvec;
         ra.n = S;
-        if (const size_t nsc = reduce_rows_scratch(ra.w, ra.q))  // constants beyond the LDS: global
+        ra.lds_max = ctx->lds_per_block;
+        if (const size_t nsc = reduce_rows_scratch(ra.w, ra.q, ra.lds_max))  // constants beyond the LDS: global
             ra.consts29 = (F29*)ctx->buf("o_rr_consts", nsc * sizeof(F29));
         LSP_HIP(launch_reduce_rows(ra, st));
         T.end("reduce rows");

@@ -25,3 +25,24 @@ def test_parsers_under_asan_ubsan(oracle_lib, tmp_path, log_n, ncols, seed):
                        capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert "sanitize ok" in r.stdout
+
+
+@pytest.mark.skipif(shutil.which("/opt/rocm/bin/hipcc") is None, reason="needs hipcc")
+def test_debug_bounds_build(product_lib):
+    """SURVEY 5's bounds-checked debug kernels: build.py --debug-bounds
+    compiles every kernel with LSP_DEBUG_BOUNDS (csrc/dbg_bounds.hpp) into
+    liblsp_hip_dbg.so, which exports the product's symbols and names itself;
+    tests/test_gpu_debug_bounds.py runs it on the GPU"""
+    import ctypes
+    from linea_stark_prover_amd import _lib
+    from linea_stark_prover_amd import build as B
+    lib_path = B.build(verbose=False, debug_bounds=True)
+    assert os.path.basename(lib_path) == "liblsp_hip_dbg.so"
+    code = ("import ctypes, sys; L = ctypes.CDLL(sys.argv[1]); L.lsp_version.restype = ctypes.c_char_p; "
+            "print(L.lsp_version().decode()); "
+            "[getattr(L, n) for n in sys.argv[2:]]")
+    r = subprocess.run([os.sys.executable, "-c", code, lib_path] + list(_lib.EXPORTED), capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "debug-bounds" in r.stdout
+    product_lib.lsp_version.restype = ctypes.c_char_p
+    assert b"debug-bounds" not in product_lib.lsp_version()

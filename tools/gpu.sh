@@ -9,6 +9,7 @@
 #
 #   tests            every GPU test (pytest -m gpu)
 #   tests:<files>    the listed test files only, comma-separated (tests/ implied)
+#   tests-dbg:<files> the same on the bounds-checked debug library (LSP_LIB=liblsp_hip_dbg.so)
 #   smoke            __graft_entry__.smoke()
 #   bench            the default bench line (what the driver runs)
 #   benchq           a quick bench: main leg only, no CPU baseline / extra legs
@@ -36,6 +37,13 @@ for step in "$@"; do
       log=gpurun_out/tests_$TAG.log
       files=$(echo "${step#tests:}" | tr ',' '\n' | sed 's#^#tests/#' | tr '\n' ' ')
       timeout -k 10 1000 $PYT -v $files >> $log 2>&1 || fail "$step" $log
+      grep -E "passed|failed" $log | tail -1 ;;
+    tests-dbg:*)
+      # the listed GPU test files on the bounds-checked debug library (build.py --debug-bounds)
+      log=gpurun_out/tests_dbg_$TAG.log
+      files=$(echo "${step#tests-dbg:}" | tr ',' '\n' | sed 's#^#tests/#' | tr '\n' ' ')
+      LSP_LIB=$PWD/linea_stark_prover_amd/_lib/liblsp_hip_dbg.so timeout -k 10 1000 $PYT $files >> $log 2>&1 \
+        || fail "$step" $log
       grep -E "passed|failed" $log | tail -1 ;;
     smoke)
       log=gpurun_out/smoke_$TAG.log

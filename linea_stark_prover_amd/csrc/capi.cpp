@@ -41,6 +41,16 @@ std::string bounds_fault_report() {
 }
 #endif
 
+}  // namespace
+
+#ifdef LSP_DEBUG_BOUNDS
+void lsp::dbg_check_after(const char* what) {
+    const std::string bad = bounds_fault_report();
+    if (!bad.empty()) throw LspError(LSP_E_STATE, bad + " after " + what);
+}
+#endif
+
+namespace {
 template <class F>
 int guarded(lsp_ctx* ctx, F&& f) {
     try {

@@ -30,11 +30,22 @@ struct LspError : std::runtime_error {
     LspError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
 
+#ifdef LSP_DEBUG_BOUNDS
+// the debug-bounds build checks the kernels' fault words after every HIP call
+// (a device sync each), so a failed check names the launch that made it
+// (capi.cpp; dbg_bounds.hpp)
+void dbg_check_after(const char* what);  // (inside namespace lsp)
+#define LSP_DBG_AFTER(x) ::lsp::dbg_check_after(x)
+#else
+#define LSP_DBG_AFTER(x) ((void)0)
+#endif
+
 #define LSP_HIP(x)                                                                                  \
     do {                                                                                            \
         hipError_t e_ = (x);                                                                        \
         if (e_ != hipSuccess)                                                                       \
             throw ::lsp::LspError(LSP_E_HIP, std::string(#x) + " -> " + hipGetErrorString(e_)); \
+        LSP_DBG_AFTER(#x);                                                                          \
     } while (0)
 
 #define LSP_REQUIRE(cond, code, msg)                          \

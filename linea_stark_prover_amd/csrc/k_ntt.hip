@@ -450,7 +450,10 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
         for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
             uint32_t t, g, c;
             gm.split(e, t, g, c);
-            if (c >= cw) continue;
+            if (c >= cw) {  // padding columns of the last chunk: zeros (the butterflies reduce them too)
+                T.put(gm.idx(t, g, c), f29_zero());
+                continue;
+            }
             const uint32_t row = gm.row_of(t, g);
             const uint32_t srow = p.inv_gather ? brev_bits(row, p.logH) : row;
             size_t si;
@@ -499,7 +502,11 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
                 const uint32_t e = threadIdx.x + jr * NTT_THREADS;
                 uint32_t t, g, c;
                 gm.split(e, t, g, c);
-                if (e >= n_el || c >= cw) continue;
+                if (e >= n_el) continue;
+                if (c >= cw) {  // padding column: zero in the tile (never stored)
+                    T.put(gm.idx(t, g, c), f29_zero());
+                    continue;
+                }
                 F29 f;
                 if (!LSP_BOUNDS(((t << logG) + g) < (K << logG) && gm.idx(t, g, c) < n_el)) continue;
                 if (row_twist || (chain && j > 0)) {
@@ -519,7 +526,10 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
             for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
                 uint32_t t, g, c;
                 gm.split(e, t, g, c);
-                if (c >= cw) continue;
+                if (c >= cw) {  // padding columns of the last chunk: zeros (the butterflies reduce them too)
+                    T.put(gm.idx(t, g, c), f29_zero());
+                    continue;
+                }
                 const uint32_t row = gm.row_of(t, g);
                 if (!LSP_BOUNDS(row < H && gm.idx(t, g, c) < n_el && c0 + c < p.w)) continue;
                 F29 v;

@@ -84,14 +84,20 @@ struct Reader {
 };
 }  // namespace
 
-std::vector<uint8_t> serialize(const lsp_proof& p) {
+std::vector<uint8_t> serialize(const lsp_proof& p, HostPool* pool) {
     size_t nfr = 3 + p.tl.size() + p.tn.size() + p.qc.size() + p.roots.size() + p.final_poly.size(), nu32 = 6;
-    for (auto& q : p.queries) {
-        nfr += q.trow.size() + q.tpath.size() + q.qrow.size() + q.qpath.size() + q.sib.size();
-        for (auto& f : q.fpath) nfr += f.size();
-        nu32 += 2 + q.sib.size();
+    // byte offset of every query's record (queries are written independently)
+    std::vector<size_t> qoff(p.queries.size() + 1);
+    size_t qbytes = 0;
+    for (size_t i = 0; i < p.queries.size(); ++i) {
+        const auto& q = p.queries[i];
+        size_t f = q.trow.size() + q.tpath.size() + q.qrow.size() + q.qpath.size() + q.sib.size(), u = 2 + q.sib.size();
+        for (auto& fp : q.fpath) f += fp.size();
+        qoff[i] = qbytes;
+        qbytes += 32 * f + 4 * u;
     }
-    std::vector<uint8_t> b(8 + 4 * nu32 + 32 * nfr);
+    const size_t head = 8 + 4 * nu32 + 32 * nfr;  // header + the fields before the queries
+    std::vector<uint8_t> b(head + qbytes);
     std::memcpy(b.data(), "LSPPRF02", 8);
     Writer w{b.data() + 8};
     w.u32(p.log_h);
@@ -108,20 +114,26 @@ std::vector<uint8_t> serialize(const lsp_proof& p) {
     w.frs(p.roots);
     w.frs(p.final_poly);
     w.fr(p.pow_w);
-    for (auto& q : p.queries) {
-        w.frs(q.trow);
-        w.u32((uint32_t)q.tpath.size());
-        w.frs(q.tpath);
-        w.frs(q.qrow);
-        w.u32((uint32_t)q.qpath.size());
-        w.frs(q.qpath);
+    if (w.p != b.data() + head) throw LspError(LSP_E_STATE, "proof serialization size mismatch");
+    auto write_query = [&](size_t i) {
+        const auto& q = p.queries[i];
+        Writer wq{b.data() + head + qoff[i]};
+        wq.frs(q.trow);
+        wq.u32((uint32_t)q.tpath.size());
+        wq.frs(q.tpath);
+        wq.frs(q.qrow);
+        wq.u32((uint32_t)q.qpath.size());
+        wq.frs(q.qpath);
         for (size_t r = 0; r < q.sib.size(); ++r) {
-            w.fr(q.sib[r]);
-            w.u32((uint32_t)q.fpath[r].size());
-            w.frs(q.fpath[r]);
+            wq.fr(q.sib[r]);
+            wq.u32((uint32_t)q.fpath[r].size());
+            wq.frs(q.fpath[r]);
         }
-    }
-    if (w.p != b.data() + b.size()) throw LspError(LSP_E_STATE, "proof serialization size mismatch");
+    };
+    if (pool && p.queries.size() > 1)
+        pool->parallel_for(p.queries.size(), write_query);
+    else
+        for (size_t i = 0; i < p.queries.size(); ++i) write_query(i);
     return b;
 }
 

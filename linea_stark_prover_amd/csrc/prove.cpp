@@ -388,35 +388,34 @@ static void host_compress_level(lsp_ctx* ctx, const Fr* in, Fr* out, size_t half
 // The levels above `first` digests host[0, first): each level is appended
 // after the one below it; returns the end of the layers (the root is
 // host[end - 1]).  *t_first (if given) is set after the first level.
-// Wide levels go level by level through the pool (work shared dynamically).
-// Once a level holds at most 16 digests per pool thread, the rest of the tree
-// is P = n / 16 subtrees of 16 digests, one task each (no barrier between their
-// levels: a parallel_for costs ~5 us, more than an 8-lane IFMA batch), and the
-// levels above the P subtree roots run on this thread.  The workers are awake
-// then (they just ran the level below).  LSP_HOST_SUBTREE=0: level by level.
+// pairs (optional): the `first` digests are made first, as the 2-element
+// leaves compress(pairs[2i], pairs[2i+1]) of a FRI round (A4/A5), inside the
+// same tasks.
+// The tree splits into P = (pool threads, a power of two) subtrees of
+// first / P digests, one task each: a task hashes its leaves and every level
+// of its subtree with no barrier in between (a parallel_for costs ~5 us, as
+// much as an 8-lane IFMA batch, and the levels below 16 digests per thread
+// used to take one each), and the log2 P levels above the subtree roots run on
+// this thread.  Each task keeps >= 16 digests (fewer threads for small
+// trees).  LSP_HOST_SUBTREE=0: level by level, one parallel_for each.
 static size_t host_levels(lsp_ctx* ctx, Fr* host, size_t first,
-                          std::chrono::steady_clock::time_point* t_first = nullptr) {
+                          std::chrono::steady_clock::time_point* t_first = nullptr, const Fr* pairs = nullptr) {
     static const bool subtrees = [] {
         const char* e = std::getenv("LSP_HOST_SUBTREE");
         return !(e && *e == '0');
     }();
-    constexpr size_t SUB = 16;  // digests per subtree task
     HostPool& pool = ctx->host_pool();
-    size_t lo = 0, n = first, end = first;
-    while (n > 1 && (!subtrees || n > SUB * pool.size())) {
-        host_compress_level(ctx, host + lo, host + end, n / 2);
-        if (lo == 0 && t_first) *t_first = std::chrono::steady_clock::now();
-        lo = end;
-        end += n / 2;
-        n /= 2;
+    if (first <= 1) {
+        if (pairs && first == 1) host[0] = ctx->p2.compress(pairs[0], pairs[1]);
+        if (t_first) *t_first = std::chrono::steady_clock::now();
+        return first;
     }
-    if (n <= 1) return end;
-    // n (a power of two, <= SUB * threads) digests at host[lo, lo + n): level
-    // j >= 1 above them holds n >> j digests at off[j]
+    // level j >= 0 holds first >> j digests at off[j]
     size_t off[64];
     uint32_t nl = 0;
-    off[0] = lo;
-    for (size_t c = n / 2; c >= 1; c /= 2) {
+    off[0] = 0;
+    size_t end = first;
+    for (size_t c = first / 2; c >= 1; c /= 2) {
         off[++nl] = end;
         end += c;
     }
@@ -426,13 +425,34 @@ static size_t host_levels(lsp_ctx* ctx, Fr* host, size_t first,
         else
             ctx->p2.compress_range(host + off[j - 1], host + off[j], i0, i0 + cnt);
     };
-    const uint32_t sl = n >= SUB ? log2_exact(SUB) : 0;  // levels inside a subtree task
-    if (sl)
-        pool.parallel_for(n / SUB, [&](size_t p) {
-            for (uint32_t j = 1; j <= sl; ++j) level_part(j, p * (SUB >> j), SUB >> j);
-        });
-    for (uint32_t j = sl + 1; j <= nl; ++j) level_part(j, 0, n >> j);  // above the subtree roots
-    if (lo == 0 && t_first) *t_first = std::chrono::steady_clock::now();
+    auto leaf_part = [&](size_t i0, size_t cnt) {
+        if (cnt == 1)
+            host[i0] = ctx->p2.compress(pairs[2 * i0], pairs[2 * i0 + 1]);
+        else
+            ctx->p2.compress_range(pairs, host, i0, i0 + cnt);
+    };
+    if (!subtrees) {
+        if (pairs) host_compress_level(ctx, pairs, host, first);
+        for (uint32_t j = 1; j <= nl; ++j) {
+            host_compress_level(ctx, host + off[j - 1], host + off[j], first >> j);
+            if (j == 1 && t_first) *t_first = std::chrono::steady_clock::now();
+        }
+        return end;
+    }
+    size_t P = 1;
+    while (2 * P <= pool.size() && first / (2 * P) >= 16) P *= 2;
+    const size_t per = first / P;
+    const uint32_t sl = log2_exact(per);  // levels inside a task
+    auto task = [&](size_t p) {
+        if (pairs) leaf_part(p * per, per);
+        for (uint32_t j = 1; j <= sl; ++j) level_part(j, p * (per >> j), per >> j);
+    };
+    if (P > 1)
+        pool.parallel_for(P, task);
+    else
+        task(0);
+    if (t_first) *t_first = std::chrono::steady_clock::now();
+    for (uint32_t j = sl + 1; j <= nl; ++j) level_part(j, 0, first >> j);  // above the task roots
     return end;
 }
 
@@ -1120,9 +1140,9 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                     const Fr* v = hv + hvo;
                     Fr* lay = htr + hto;
                     const auto tr0 = std::chrono::steady_clock::now();
-                    host_compress_level(ctx, v, lay, m);  // a 2-element leaf's hash_iter is compress (A4/A5)
-                    const auto tr1 = std::chrono::steady_clock::now();
-                    const size_t end = host_levels(ctx, lay, m);
+                    // leaves (a 2-element leaf's hash_iter is compress, A4/A5) and levels in one pass
+                    auto tr1 = tr0;
+                    const size_t end = host_levels(ctx, lay, m, &tr1, v);
                     const auto tr2 = std::chrono::steady_clock::now();
                     FriRound R;
                     R.vec = fv + vo;
@@ -1317,11 +1337,13 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         auto top_path = [&](const std::vector<std::vector<Fr>>& top, size_t sub, std::vector<Fr>& out) {
             for (uint32_t i = 0; i + 1 < top.size(); ++i) out.push_back(top[i][(sub >> i) ^ 1]);
         };
-        proof->queries.reserve(nq);
-        for (uint32_t qi = 0; qi < nq; ++qi) {
+        // each query's record is independent: assembled (and below serialized)
+        // on the host pool -- ~0.1 + 0.2 ms of one thread's time at 2^19
+        proof->queries.resize(nq);
+        ctx->host_pool().parallel_for(nq, [&](size_t qi) {
             const size_t idx = idxs[qi], o = idx >> logS;
             const Fr* e = all.data() + (o * nq + qi) * E;
-            lsp_query qq;
+            lsp_query& qq = proof->queries[qi];
             qq.sib.reserve(nr);
             qq.fpath.reserve(nr);
             qq.trow.assign(e, e + w);
@@ -1343,8 +1365,9 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                 if (R.sharded) top_path(R.top, o, pth);
                 qq.fpath.push_back(std::move(pth));
             }
-            proof->queries.push_back(std::move(qq));
-        }
+        });
+        // the wire bytes now, in parallel (lsp_proof_serialize returns the cached copy)
+        proof->wire = serialize(*proof, &ctx->host_pool());
         const auto q3 = std::chrono::steady_clock::now();
         T.end("query phase");
         T.end("FRI prover");

@@ -26,7 +26,9 @@ struct Comm;
 lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, size_t w, const Air& air,
                        const Fr* pub, size_t npub);
 // proof wire format and field view (proof.cpp)
-std::vector<uint8_t> serialize(const lsp_proof& p);
+// pool (optional): the queries are written in parallel (the element
+// conversions to canonical words are ~2/3 of a 2^19 proof's 10 K elements)
+std::vector<uint8_t> serialize(const lsp_proof& p, HostPool* pool = nullptr);
 lsp_proof* deserialize(const uint8_t* buf, size_t len);
 void proof_view(const lsp_proof& p, lsp_proof_view* v);
 lsp_proof* proof_from_view(const lsp_proof_view& v);

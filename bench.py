@@ -292,6 +292,8 @@ def main_leg(args, dist, ranks_seen):
     if rank == 0 and args.dump_proof and proof is not None:
         with open(args.dump_proof, "wb") as f:
             f.write(proof)
+    # one process per rank: every collective of the last proof, per rank (lsp_comm_log)
+    table = collective_table(ctx, dist) if shard and world > 1 else None
     comm = getattr(ctx, "_comm", None)
     if args.dump_comm_schedule and comm is not None:
         with open(f"{args.dump_comm_schedule}.{rank}.json", "w") as f:
@@ -386,6 +388,8 @@ def main_leg(args, dist, ranks_seen):
                               "valu_issue_source": VALU_SRC.get("src"),
                               "perms": trace_perms, "fr_mul_per_perm": FR_MUL_PER_PERM, "ms": merkle_ms},
         }
+        if table is not None:
+            out.update(table)
         if world == 1 and not shard and args.inflight > 1:
             out["inflight"] = inflight(args, cfg, air, pub, trace, ctx, dtrace)
         if world == 1 and not shard and not args.no_host_trace_leg:

@@ -225,9 +225,12 @@ void lde_device(lsp_ctx* ctx, const Fr* d_in, size_t h, size_t w, uint32_t added
     LSP_REQUIRE(k0 + nk <= B, LSP_E_ARG, "coset range outside the LDE");
     LSP_REQUIRE(logh + added_bits <= 47, LSP_E_SIZE, "LDE larger than the 2-adic subgroup");
     Fr* X = ctx->fbuf("lde_X", h * w);
-    const TwistTables T = lde_twist(ctx, h, w, added_bits, shifts_host, k0, nk);
+    // with the chained twist the fused pass reads only block k0's table (the
+    // later blocks multiply by rho^row), so only that one is built and cached
+    const Fr* ratio = chain_ratio(ctx, logh, added_bits, k0, nk);
+    const TwistTables T = lde_twist(ctx, h, w, added_bits, shifts_host, k0, ratio ? 1 : nk);
     LSP_HIP(launch_lde(d_in, X, d_out, w, logh, nk, ctx->twiddle29(logh, true), ctx->twiddle29(logh, false), T.tabs,
-                       T.L1, T.L2, T.shared ? 0 : 1, chain_ratio(ctx, logh, added_bits, k0, nk), ctx->stream));
+                       T.L1, T.L2, T.shared ? 0 : 1, ratio, ctx->stream));
 }
 
 // The same blocks from h * coefficients (natural order) at `coef`, laid out
@@ -236,9 +239,10 @@ static void lde_coeffs_device(lsp_ctx* ctx, const Fr* coef, ColMap map, size_t h
                               const Fr* shifts_host, Fr* d_out, uint32_t k0, uint32_t nk, bool div_h = true) {
     const uint32_t logh = log2_exact(h);
     LSP_REQUIRE(k0 + nk <= (1u << added_bits) && logh >= 1, LSP_E_ARG, "coset range outside the LDE");
-    const TwistTables T = lde_twist(ctx, h, w, added_bits, shifts_host, k0, nk, div_h);
+    const Fr* ratio = chain_ratio(ctx, logh, added_bits, k0, nk);  // (block k0's table only, as lde_device)
+    const TwistTables T = lde_twist(ctx, h, w, added_bits, shifts_host, k0, ratio ? 1 : nk, div_h);
     LSP_HIP(launch_lde_coeffs(coef, map, d_out, w, logh, nk, ctx->twiddle29(logh, false), T.tabs, T.L1, T.L2,
-                              T.shared ? 0 : 1, chain_ratio(ctx, logh, added_bits, k0, nk), ctx->stream));
+                              T.shared ? 0 : 1, ratio, ctx->stream));
 }
 
 // TwoAdicSubgroupDft::coset_dft_batch ([EXT p3-dft]; dft_batch: shift 1): the

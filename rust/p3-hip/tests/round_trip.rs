@@ -1,14 +1,14 @@
 //! A GPU proof checked by the reference's own verifier, unchanged.
 //!
 //! The config is built exactly as `bin/src/main.rs:49-78` builds it, with the
-//! one change INTEGRATION.md section 4 describes at `main.rs:49`: the
+//! one change INTEGRATION.md section 3 describes at `main.rs:49`: the
 //! Poseidon2 constants come from `p3_hip::Params::from_rng` (the draws
 //! `Perm::new_from_rng(8, 22, &mut rng)` would make) and `perm` is
 //! `p3_hip::perm(&params)`, so the Mmcs and the challenger hash with the
 //! constants the library proves with.  The AIR is the reference's `air`
 //! crate; the proof goes through `p3_uni_stark::verify` (`main.rs:88-96`).
 //! Needs a GPU and LSP_LIB_DIR (see build.rs); the Python twins are
-//! tests/test_proof_view.py and tests/test_gpu_linear_layers.py.
+//! tests/test_proof_view.py and tests/test_linear_layers.py (its GPU cases).
 use air::air_permutation::AirPermutationConfig;
 use air::{AirConfig, LineaAIR};
 use p3_bls12_377_fr::Poseidon2Bls12337;

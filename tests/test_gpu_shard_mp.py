@@ -25,6 +25,16 @@ def _run(tmp_path, nproc, comm, port, log_n=10, schedules=None):
            "--warmup", "0", "--no-cpu-baseline", "--dump-proof", str(out), "--dump-comm-schedule", str(sched)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    if nproc > 1:  # the per-collective table of the JSON line (lsp_comm_log on every rank)
+        import json
+        o = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+        assert o["schedule_identical"] is True and len(o["comm_init_ms_by_rank"]) == nproc
+        rows = o["collectives"]
+        assert rows and all(len(x["ms_by_rank"]) == nproc and x["op"] in ("allgather", "bcast") for x in rows)
+        assert {"trace coefficients", "query openings"} <= {x["tag"] for x in rows}
+        if schedules is not None and comm == "gloo":  # the library's log = the transport's own record
+            lib_sched = [(x["op"], x["bytes"], x["root"]) for x in rows]
+            assert len(lib_sched) >= 5
     if schedules is not None and comm == "gloo":
         import json
         for rk in range(nproc):
@@ -96,7 +106,7 @@ def test_bench_sharded_leg_two_ranks():
     (gloo, sharing one GPU) verifies; the replicas value beside it is weak scaling"""
     o = _bench_json(["--gpus", "2", "--log-n", "10", "--steps", "1", "--warmup", "1", "--no-cpu-baseline",
                      "--shard-leg", "12,13", "--shard-leg-steps", "1", "--shard-leg-warmup", "0",
-                     "--batch-leg", "11", "--batch-leg-steps", "1"])
+                     "--batch-leg", "11", "--batch-leg-steps", "1", "--shape-pow-bits", "0"])
     assert o["n_gpus"] == 2 and o["scaling"] == "weak" and o["verified"] is True
     b = o["batch"]["runs"][0]  # configs[4]'s shape: one independent proof per rank
     assert b["log_n"] == 11 and b["verified"] is True and b["scaling"] == "weak"
@@ -104,12 +114,17 @@ def test_bench_sharded_leg_two_ranks():
     assert sh["comm"] == "gloo" and sh["n_ranks_seen"] == 2, sh
     assert [r["log_n"] for r in sh["runs"]] == [12, 13]
     assert all(r["verified"] for r in sh["runs"])
+    for r in sh["runs"]:  # every collective, per rank, with its device time
+        assert r["schedule_identical"] is True and len(r["comm_init_ms_by_rank"]) == 2
+        assert r["collectives"] and all(len(x["ms_by_rank"]) == 2 for x in r["collectives"])
+        assert "trace coefficients" in r["collectives_by_tag"]
 
 
 def test_bench_sharded_leg_single_gpu_equals_prove():
     """N = 1: the sharded field is lsp_prove itself (prove_shard over SoloComm),
     and the device-generated trace proves and verifies"""
     o = _bench_json(["--log-n", "10", "--steps", "1", "--warmup", "1", "--no-cpu-baseline", "--inflight", "0",
+                     "--shape-pow-bits", "0",
                      "--shard-leg", "14", "--shard-leg-steps", "2", "--batch-leg", "none"])
     sh = o["sharded"]
     assert sh["comm"] == "solo" and sh["n_ranks_seen"] == 1

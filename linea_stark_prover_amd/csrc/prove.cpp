@@ -389,6 +389,56 @@ static void host_compress_level(lsp_ctx* ctx, const Fr* in, Fr* out, size_t half
     }
 }
 
+// Round 3's host levels (LSP_HOST_LEVELS=r3, for same-box A/B): level by
+// level while a level has more than 16 digests per thread, then subtrees of 16.
+// Wide levels go level by level through the pool (work shared dynamically).
+// Once a level holds at most 16 digests per pool thread, the rest of the tree
+// is P = n / 16 subtrees of 16 digests, one task each (no barrier between their
+// levels: a parallel_for costs ~5 us, more than an 8-lane IFMA batch), and the
+// levels above the P subtree roots run on this thread.  The workers are awake
+// then (they just ran the level below).  LSP_HOST_SUBTREE=0: level by level.
+static size_t host_levels_r3(lsp_ctx* ctx, Fr* host, size_t first,
+                             std::chrono::steady_clock::time_point* t_first) {
+    static const bool subtrees = [] {
+        const char* e = std::getenv("LSP_HOST_SUBTREE");
+        return !(e && *e == '0');
+    }();
+    constexpr size_t SUB = 16;  // digests per subtree task
+    HostPool& pool = ctx->host_pool();
+    size_t lo = 0, n = first, end = first;
+    while (n > 1 && (!subtrees || n > SUB * pool.size())) {
+        host_compress_level(ctx, host + lo, host + end, n / 2);
+        if (lo == 0 && t_first) *t_first = std::chrono::steady_clock::now();
+        lo = end;
+        end += n / 2;
+        n /= 2;
+    }
+    if (n <= 1) return end;
+    // n (a power of two, <= SUB * threads) digests at host[lo, lo + n): level
+    // j >= 1 above them holds n >> j digests at off[j]
+    size_t off[64];
+    uint32_t nl = 0;
+    off[0] = lo;
+    for (size_t c = n / 2; c >= 1; c /= 2) {
+        off[++nl] = end;
+        end += c;
+    }
+    auto level_part = [&](uint32_t j, size_t i0, size_t cnt) {  // level j, digests [i0, i0 + cnt)
+        if (cnt == 1)
+            host[off[j] + i0] = ctx->p2.compress(host[off[j - 1] + 2 * i0], host[off[j - 1] + 2 * i0 + 1]);
+        else
+            ctx->p2.compress_range(host + off[j - 1], host + off[j], i0, i0 + cnt);
+    };
+    const uint32_t sl = n >= SUB ? log2_exact(SUB) : 0;  // levels inside a subtree task
+    if (sl)
+        pool.parallel_for(n / SUB, [&](size_t p) {
+            for (uint32_t j = 1; j <= sl; ++j) level_part(j, p * (SUB >> j), SUB >> j);
+        });
+    for (uint32_t j = sl + 1; j <= nl; ++j) level_part(j, 0, n >> j);  // above the subtree roots
+    if (lo == 0 && t_first) *t_first = std::chrono::steady_clock::now();
+    return end;
+}
+
 // The levels above `first` digests host[0, first): each level is appended
 // after the one below it; returns the end of the layers (the root is
 // host[end - 1]).  *t_first (if given) is set after the first level.
@@ -409,6 +459,10 @@ static size_t host_levels(lsp_ctx* ctx, Fr* host, size_t first,
         return !(e && *e == '0');
     }();
     HostPool& pool = ctx->host_pool();
+    if (const char* e = std::getenv("LSP_HOST_LEVELS"); e && e[0] == 'r') {  // A/B: round 3's levels
+        if (pairs) host_compress_level(ctx, pairs, host, first);
+        return host_levels_r3(ctx, host, first, t_first);
+    }
     if (first <= 1) {
         if (pairs && first == 1) host[0] = ctx->p2.compress(pairs[0], pairs[1]);
         if (t_first) *t_first = std::chrono::steady_clock::now();
@@ -1344,7 +1398,10 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         // each query's record is independent: assembled (and below serialized)
         // on the host pool -- ~0.1 + 0.2 ms of one thread's time at 2^19
         proof->queries.resize(nq);
-        ctx->host_pool().parallel_for(nq, [&](size_t qi) {
+        const char* qp = std::getenv("LSP_QUERY_POOL");  // =0: one thread, wire bytes on demand (A/B)
+        const bool qpool = !(qp && *qp == '0');
+        HostPool serial_pool(0);
+        (qpool ? ctx->host_pool() : serial_pool).parallel_for(nq, [&](size_t qi) {
             const size_t idx = idxs[qi], o = idx >> logS;
             const Fr* e = all.data() + (o * nq + qi) * E;
             lsp_query& qq = proof->queries[qi];
@@ -1371,7 +1428,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             }
         });
         // the wire bytes now, in parallel (lsp_proof_serialize returns the cached copy)
-        proof->wire = serialize(*proof, &ctx->host_pool());
+        if (qpool) proof->wire = serialize(*proof, &ctx->host_pool());
         const auto q3 = std::chrono::steady_clock::now();
         T.end("query phase");
         T.end("FRI prover");

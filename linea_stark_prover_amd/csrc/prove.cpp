@@ -750,6 +750,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                        const Fr* pub, size_t npub) {
     LSP_REQUIRE(npub >= 2, LSP_E_ARG, "public values must hold [alpha, delta]");
     LSP_REQUIRE(air.max_col < w, LSP_E_ARG, "AIR column id outside the trace width");
+    const auto t_entry = std::chrono::steady_clock::now();
     const ActiveProof active;
     const DeferTopUploads defer(ctx);
     comm.begin_log(ctx);
@@ -830,6 +831,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             lde_coeffs_device(ctx, tcoef, tmap, h, w, lb, shifts.data(), lde, k0, nk);
         else
             lde_device(ctx, d_trace, h, w, lb, shifts.data(), lde, k0, nk);
+        const auto t_lde_issued = std::chrono::steady_clock::now();
         T.end("coset_lde_batch");
         Fr* tlay = ctx->fbuf("t_tree", 2 * S - 1);
         std::vector<std::vector<Fr>> ttop, qtop;
@@ -1435,7 +1437,13 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         T.end("open");
         T.end("prove");
         T.collect();
-        if (g_top_times.on) { const auto q4 = std::chrono::steady_clock::now(); std::fprintf(stderr, "[query] samples %.1f us, gather+sync %.1f us, assemble %.1f us, collect %.1f us\n", std::chrono::duration<double, std::micro>(q1 - q0).count(), std::chrono::duration<double, std::micro>(q2 - q1).count(), std::chrono::duration<double, std::micro>(q3 - q2).count(), std::chrono::duration<double, std::micro>(q4 - q3).count()); }
+        if (g_top_times.on) {
+            const auto q4 = std::chrono::steady_clock::now();
+            auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+            std::fprintf(stderr, "[query] samples %.1f us, gather+sync %.1f us, assemble %.1f us, collect %.1f us; "
+                                 "entry -> LDE issued %.1f us\n",
+                         us(q0, q1), us(q1, q2), us(q2, q3), us(q3, q4), us(t_entry, t_lde_issued));
+        }
     } catch (...) {
         delete proof;
         throw;

@@ -1076,7 +1076,7 @@ int lsp_proof_from_view(const lsp_proof_view* view, lsp_proof** out) {
 }
 
 int lsp_proof_free(lsp_proof* p) {
-    delete p;
+    proof_release(p);  // its wire bytes and query records are reused by the next proof
     return LSP_OK;
 }
 

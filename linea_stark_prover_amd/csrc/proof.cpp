@@ -13,7 +13,9 @@
 // produced elsewhere, for lsp_verify).  Everything here is host code and
 // treats its input bytes as untrusted (tests/test_proof_view.py fuzzes it,
 // tools/sanitize builds it under ASan/UBSan).
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 #include "prove_internal.hpp"
 
@@ -84,7 +86,61 @@ struct Reader {
 };
 }  // namespace
 
-std::vector<uint8_t> serialize(const lsp_proof& p, HostPool* pool) {
+namespace {
+struct Recycler {
+    std::mutex mu;
+    std::vector<std::vector<uint8_t>> wires;
+    std::vector<std::vector<lsp_query>> queries;
+    static constexpr size_t KEEP = 4;  // proofs' worth held at most
+};
+Recycler& recycler() {
+    static Recycler* r = new Recycler();  // never destroyed: frees may run during exit
+    return *r;
+}
+}  // namespace
+
+// LSP_RECYCLE=0: plain frees and fresh allocations (same-box A/B; read per call)
+static bool recycle_on() {
+    const char* e = std::getenv("LSP_RECYCLE");
+    return !(e && *e == '0');
+}
+
+void proof_release(lsp_proof* p) {
+    if (!p) return;
+    if (!recycle_on()) {
+        delete p;
+        return;
+    }
+    Recycler& r = recycler();
+    {
+        std::lock_guard<std::mutex> g(r.mu);
+        if (r.wires.size() < Recycler::KEEP && p->wire.capacity() > 0) r.wires.push_back(std::move(p->wire));
+        if (r.queries.size() < Recycler::KEEP && p->queries.capacity() > 0) r.queries.push_back(std::move(p->queries));
+    }
+    delete p;
+}
+
+std::vector<uint8_t> recycled_wire() {
+    if (!recycle_on()) return {};
+    Recycler& r = recycler();
+    std::lock_guard<std::mutex> g(r.mu);
+    if (r.wires.empty()) return {};
+    std::vector<uint8_t> v = std::move(r.wires.back());
+    r.wires.pop_back();
+    return v;
+}
+
+std::vector<lsp_query> recycled_queries() {
+    if (!recycle_on()) return {};
+    Recycler& r = recycler();
+    std::lock_guard<std::mutex> g(r.mu);
+    if (r.queries.empty()) return {};
+    std::vector<lsp_query> v = std::move(r.queries.back());
+    r.queries.pop_back();
+    return v;
+}
+
+std::vector<uint8_t> serialize(const lsp_proof& p, HostPool* pool, std::vector<uint8_t>* reuse) {
     size_t nfr = 3 + p.tl.size() + p.tn.size() + p.qc.size() + p.roots.size() + p.final_poly.size(), nu32 = 6;
     // byte offset of every query's record (queries are written independently)
     std::vector<size_t> qoff(p.queries.size() + 1);
@@ -97,7 +153,11 @@ std::vector<uint8_t> serialize(const lsp_proof& p, HostPool* pool) {
         qbytes += 32 * f + 4 * u;
     }
     const size_t head = 8 + 4 * nu32 + 32 * nfr;  // header + the fields before the queries
-    std::vector<uint8_t> b(head + qbytes);
+    std::vector<uint8_t> b;
+    if (reuse) b.swap(*reuse);
+    // every byte is written below, so a recycled buffer needs no clearing
+    // (resize value-initialises only what it adds)
+    b.resize(head + qbytes);
     std::memcpy(b.data(), "LSPPRF02", 8);
     Writer w{b.data() + 8};
     w.u32(p.log_h);

@@ -1382,12 +1382,24 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         LSP_REQUIRE(ptrs.size() == mine.size() * E, LSP_E_STATE, "query opening layout mismatch");
         std::vector<Fr> slots((size_t)nq * E, fr_zero());
         if (!ptrs.empty()) {
-            uint64_t* dptrs = (uint64_t*)ctx->buf("g_ptrs", ptrs.size() * sizeof(uint64_t));
-            Fr* dgot = ctx->fbuf("g_out", ptrs.size());
-            ctx->h2d_async("g_ptrs_h", dptrs, ptrs.data(), ptrs.size() * sizeof(uint64_t));
-            LSP_HIP(launch_gather(dptrs, dgot, ptrs.size(), st));
-            Fr* got = (Fr*)ctx->hbuf("g_out_h", ptrs.size() * sizeof(Fr));  // pinned: no staging copy
-            LSP_HIP(hipMemcpyAsync(got, dgot, ptrs.size() * sizeof(Fr), hipMemcpyDeviceToHost, st));
+            // the gather reads its pointer list from pinned host memory and writes the
+            // openings into coherent pinned memory: no copy either side of the kernel
+            // (LSP_GATHER_ZEROCOPY=0: upload, gather to HBM, download; read per call)
+            const char* zc = std::getenv("LSP_GATHER_ZEROCOPY");
+            Fr* got;
+            if (!(zc && *zc == '0')) {
+                uint64_t* hp = (uint64_t*)ctx->hbuf("g_ptrs_zc", ptrs.size() * sizeof(uint64_t));
+                std::memcpy(hp, ptrs.data(), ptrs.size() * sizeof(uint64_t));
+                got = (Fr*)ctx->hbuf("g_out_zc", ptrs.size() * sizeof(Fr), hipHostMallocCoherent);
+                LSP_HIP(launch_gather(hp, got, ptrs.size(), st));
+            } else {
+                uint64_t* dptrs = (uint64_t*)ctx->buf("g_ptrs", ptrs.size() * sizeof(uint64_t));
+                Fr* dgot = ctx->fbuf("g_out", ptrs.size());
+                ctx->h2d_async("g_ptrs_h", dptrs, ptrs.data(), ptrs.size() * sizeof(uint64_t));
+                LSP_HIP(launch_gather(dptrs, dgot, ptrs.size(), st));
+                got = (Fr*)ctx->hbuf("g_out_h", ptrs.size() * sizeof(Fr));  // pinned: no staging copy
+                LSP_HIP(hipMemcpyAsync(got, dgot, ptrs.size() * sizeof(Fr), hipMemcpyDeviceToHost, st));
+            }
             LSP_HIP(hipStreamSynchronize(st));
             for (size_t k = 0; k < mine.size(); ++k)
                 std::copy(got + k * E, got + (k + 1) * E, slots.begin() + (size_t)mine[k] * E);
@@ -1399,6 +1411,8 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         };
         // each query's record is independent: assembled (and below serialized)
         // on the host pool -- ~0.1 + 0.2 ms of one thread's time at 2^19
+        // records of a freed proof keep their vectors' capacity (proof_release)
+        proof->queries = recycled_queries();
         proof->queries.resize(nq);
         const char* qp = std::getenv("LSP_QUERY_POOL");  // =0: one thread, wire bytes on demand (A/B)
         const bool qpool = !(qp && *qp == '0');
@@ -1407,8 +1421,9 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             const size_t idx = idxs[qi], o = idx >> logS;
             const Fr* e = all.data() + (o * nq + qi) * E;
             lsp_query& qq = proof->queries[qi];
+            qq.sib.clear();
             qq.sib.reserve(nr);
-            qq.fpath.reserve(nr);
+            qq.fpath.resize(nr);
             qq.trow.assign(e, e + w);
             e += w;
             qq.tpath.assign(e, e + logS);
@@ -1423,14 +1438,17 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                 const FriRound& R = rounds[r];
                 qq.sib.push_back(*e++);
                 const uint32_t lg = log2_exact(R.ml);
-                std::vector<Fr> pth(e, e + lg);
+                std::vector<Fr>& pth = qq.fpath[r];
+                pth.assign(e, e + lg);
                 e += lg;
                 if (R.sharded) top_path(R.top, o, pth);
-                qq.fpath.push_back(std::move(pth));
             }
         });
         // the wire bytes now, in parallel (lsp_proof_serialize returns the cached copy)
-        if (qpool) proof->wire = serialize(*proof, &ctx->host_pool());
+        if (qpool) {
+            std::vector<uint8_t> buf = recycled_wire();
+            proof->wire = serialize(*proof, &ctx->host_pool(), &buf);
+        }
         const auto q3 = std::chrono::steady_clock::now();
         T.end("query phase");
         T.end("FRI prover");

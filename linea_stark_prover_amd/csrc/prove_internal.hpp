@@ -28,8 +28,16 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
 // proof wire format and field view (proof.cpp)
 // pool (optional): the queries are written in parallel (the element
 // conversions to canonical words are ~2/3 of a 2^19 proof's 10 K elements)
-std::vector<uint8_t> serialize(const lsp_proof& p, HostPool* pool = nullptr);
+// reuse (optional): a buffer whose allocation the result takes over
+std::vector<uint8_t> serialize(const lsp_proof& p, HostPool* pool = nullptr, std::vector<uint8_t>* reuse = nullptr);
 lsp_proof* deserialize(const uint8_t* buf, size_t len);
+// A freed proof's largest allocations -- its wire bytes (a fresh 324 KB vector
+// per 2^19 proof is an mmap, page faults and an munmap) and its query records
+// (~800 small vectors) -- go back to a small process-wide stock that the next
+// proof's query assembly and serialization take from (proof.cpp)
+void proof_release(lsp_proof* p);
+std::vector<uint8_t> recycled_wire();
+std::vector<lsp_query> recycled_queries();
 void proof_view(const lsp_proof& p, lsp_proof_view* v);
 lsp_proof* proof_from_view(const lsp_proof_view& v);
 // communicators of a process-per-GPU sharded prove (comm_ext.cpp)

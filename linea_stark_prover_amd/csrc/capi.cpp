@@ -297,6 +297,7 @@ int lsp_ctx_destroy(lsp_ctx* ctx) {
     }
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->side_stream) (void)hipStreamSynchronize(ctx->side_stream);
     for (auto& kv : ctx->pool)
         if (kv.second.p) (void)hipFree(kv.second.p);
     for (auto& kv : ctx->hpool)
@@ -310,6 +311,12 @@ int lsp_ctx_destroy(lsp_ctx* ctx) {
     }
     if (ctx->ev_near) (void)hipEventDestroy(ctx->ev_near);
     if (ctx->ev_top) (void)hipEventDestroy(ctx->ev_top);
+    if (ctx->side_stream) {
+        (void)hipStreamSynchronize(ctx->side_stream);
+        (void)hipEventDestroy(ctx->ev_wide);
+        (void)hipEventDestroy(ctx->ev_side);
+        (void)hipStreamDestroy(ctx->side_stream);
+    }
     if (ctx->rc_dev) (void)hipFree(ctx->rc_dev);
     if (ctx->rc29_dev) (void)hipFree(ctx->rc29_dev);
     (void)hipStreamDestroy(ctx->stream);

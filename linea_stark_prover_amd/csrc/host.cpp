@@ -368,6 +368,17 @@ void lsp_ctx::h2d_async(const std::string& name, void* dst, const void* src, siz
     LSP_HIP(hipEventRecord(it->second, stream));
 }
 
+hipStream_t lsp_ctx::side() {
+    if (!side_stream) {
+        int least = 0, greatest = 0;
+        LSP_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        LSP_HIP(hipStreamCreateWithPriority(&side_stream, hipStreamNonBlocking, least));
+        LSP_HIP(hipEventCreateWithFlags(&ev_wide, hipEventDisableTiming));
+        LSP_HIP(hipEventCreateWithFlags(&ev_side, hipEventDisableTiming));
+    }
+    return side_stream;
+}
+
 lsp::HostPool& lsp_ctx::host_pool() {
     if (!pool_) {
         // up to 16 threads (a 1-GPU box's CPU share), fewer when the launcher

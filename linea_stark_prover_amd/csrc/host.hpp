@@ -301,6 +301,12 @@ struct lsp_ctx {
     std::map<std::string, Buf> hpool;  // pinned host staging buffers (hbuf)
     std::map<std::string, hipEvent_t> stage_ev;  // last copy out of each h2d_async staging buffer
     hipEvent_t ev_near = nullptr, ev_top = nullptr;  // tree-top hand-off (prove.cpp commit_device)
+    // work beside a tree's narrow levels (prove.cpp, "constraints before alpha"):
+    // a low-priority stream, the event after the tree's wide levels it waits
+    // for, and the event the main stream waits for before using its results
+    hipStream_t side_stream = nullptr;
+    hipEvent_t ev_wide = nullptr, ev_side = nullptr;
+    hipStream_t side();  // side_stream, created on first use
     std::vector<hipEvent_t> event_pool;               // phase-timer events, reused across proofs
     // per-phase device timings of lsp_prove (lsp_last_timings): two events per
     // phase, ~0.3 ms of host API time per 2^19 proof; lsp_ctx_set_phase_timing

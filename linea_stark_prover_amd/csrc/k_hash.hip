@@ -105,6 +105,10 @@ __global__ __launch_bounds__(256) void k_fold_hash(FoldSpec f, size_t nleaves, F
 template <uint32_t D, int LANES>
 __global__ __launch_bounds__(256) void k_merkle_level(const Fr* __restrict__ src, Fr* __restrict__ dst, size_t nout,
                                                       const F29* __restrict__ rc, uint32_t rf, uint32_t rp) {
+    // the narrow forms are one permutation's latency per level, the critical
+    // path: their waves win the SIMD's issue arbitration against work a side
+    // stream runs beside them (prove.cpp, constraints before alpha)
+    if constexpr (LANES > 1) __builtin_amdgcn_s_setprio(3);
     __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
     f29_qtab_init(qt);
     __syncthreads();

@@ -56,6 +56,16 @@ __global__ __launch_bounds__(256) void k_selector_denoms(const Fr* __restrict__ 
     den[m] = fr_mul(fr_sub(x, fr_one()), fr_sub(x, wh_inv));
 }
 
+// one constraint value of thread t, limb-planar (QuotientArgs::cons)
+__device__ __forceinline__ void st_cons(const QuotientArgs& a, uint32_t j, size_t t, size_t n, const F29& v) {
+    if (!LSP_BOUNDS(j < a.ncons)) return;
+    uint32_t* c = a.cons + (size_t)j * 9 * n + t;
+#pragma unroll
+    for (int l = 0; l < 9; ++l) c[(size_t)l * n] = v.l[l];
+}
+
+// EARLY: write the constraint values (QuotientArgs::cons) instead of folding them
+template <bool EARLY>
 __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
     __shared__ uint4 qt[3 * F29_QTAB_N];  // f29_reduce_qt's table
     f29_qtab_init(qt);
@@ -63,7 +73,9 @@ __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
     const Q29 F{qt};
     const size_t t = gtid();
     const size_t Q = 1ull << a.logQ;
-    if (t >= (a.n ? a.n : Q)) return;  // n = Q >> log_step points
+    const size_t npts = a.n ? a.n : Q;
+    if (t >= npts) return;  // n = Q >> log_step points
+    const size_t tcons = t;  // (the lookup loop below names its table index t)
     // Row order: thread t evaluates point m = bitrev(t), whose row bitrev_Q(i)
     // is row0 + t, so a wave reads 64 adjacent LDE rows (and their
     // successors).  In point order it read rows Q/64 apart: with the C3
@@ -93,7 +105,14 @@ __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
     const Fr* nxt = (a.lde_next ? a.lde_next : a.lde) + nrow * a.w;
     const F29 ap = f29_from_fr(a.pub_alpha), dl = f29_from_fr(a.pub_delta), al = f29_from_fr(a.alpha);
     F29 acc = f29_zero();
-#define PUSH(X) acc = F.add(F.mul(acc, al), (X))
+    uint32_t ncw = 0;  // constraints written (EARLY)
+#define PUSH(X)                                     \
+    do {                                            \
+        if constexpr (EARLY)                        \
+            st_cons(a, ncw++, tcons, npts, (X));    \
+        else                                        \
+            acc = F.add(F.mul(acc, al), (X));       \
+    } while (0)
     const int32_t* d = a.air;
     int32_t p = 0;
     const int32_t ncfg = d[p++];
@@ -149,6 +168,31 @@ __global__ __launch_bounds__(256) void k_quotient(QuotientArgs a) {
         }
     }
 #undef PUSH
+    if constexpr (!EARLY) a.out[m] = f29_to_fr_qt(F.mul(acc, f29_from_fr(a.inv_zh[i & qmask])), qt);
+}
+
+// the fold of the values k_quotient<true> wrote: thread t reads its own
+// (coalesced) and writes point m as k_quotient<false> would
+__global__ __launch_bounds__(256) void k_quotient_fold(QuotientArgs a) {
+    __shared__ uint4 qt[3 * F29_QTAB_N];
+    f29_qtab_init(qt);
+    __syncthreads();
+    const Q29 F{qt};
+    const size_t t = gtid();
+    const size_t npts = a.n ? a.n : (1ull << a.logQ);
+    if (t >= npts) return;
+    const size_t m = a.row_order ? brev_bits(t, a.logQ - a.log_step) : t;
+    const uint64_t i = a.i0 + ((uint64_t)m << a.log_step);
+    const uint32_t qmask = (1u << a.log_q) - 1;
+    const F29 al = f29_from_fr(a.alpha);
+    F29 acc = f29_zero();
+    for (uint32_t j = 0; j < a.ncons; ++j) {
+        const uint32_t* c = a.cons + (size_t)j * 9 * npts + t;
+        F29 v;
+#pragma unroll
+        for (int l = 0; l < 9; ++l) v.l[l] = c[(size_t)l * npts];
+        acc = F.add(F.mul(acc, al), v);
+    }
     a.out[m] = f29_to_fr_qt(F.mul(acc, f29_from_fr(a.inv_zh[i & qmask])), qt);
 }
 }  // namespace
@@ -165,15 +209,30 @@ hipError_t launch_selector_denoms(const Fr* tabQ, uint32_t L1, Fr gen, Fr wh_inv
 // 2^19 x 8 0.475 -> 0.45 ms, 2^22 x 8 5.7 -> 3.9 ms, rank 0 of 2^26 over 8 ranks
 // 60 -> 26 ms): in point order a wave's 64 rows are Q/64 apart, and past the
 // caches' size every row is a DRAM page miss.
-hipError_t launch_quotient(const QuotientArgs& a, hipStream_t st) {
-    const size_t n = a.n ? a.n : (1ull << a.logQ);
+static QuotientArgs with_order(const QuotientArgs& a) {
     QuotientArgs b = a;
     b.row_order = 1;
     if (const char* e = std::getenv("LSP_QUOTIENT_ORDER")) {
         if (e[0] == 'r') b.row_order = 1;
         if (e[0] == 'p') b.row_order = 0;
     }
-    hipLaunchKernelGGL(k_quotient, dim3(nblocks(n, 256)), dim3(256), 0, st, b);
+    return b;
+}
+
+hipError_t launch_quotient(const QuotientArgs& a, hipStream_t st) {
+    const size_t n = a.n ? a.n : (1ull << a.logQ);
+    const QuotientArgs b = with_order(a);
+    if (a.cons)
+        hipLaunchKernelGGL(k_quotient<true>, dim3(nblocks(n, 256)), dim3(256), 0, st, b);
+    else
+        hipLaunchKernelGGL(k_quotient<false>, dim3(nblocks(n, 256)), dim3(256), 0, st, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_quotient_fold(const QuotientArgs& a, hipStream_t st) {
+    if (!a.cons) return hipErrorInvalidValue;
+    const size_t n = a.n ? a.n : (1ull << a.logQ);
+    hipLaunchKernelGGL(k_quotient_fold, dim3(nblocks(n, 256)), dim3(256), 0, st, with_order(a));
     return hipGetLastError();
 }
 

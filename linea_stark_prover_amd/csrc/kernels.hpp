@@ -207,11 +207,21 @@ struct QuotientArgs {
     uint32_t row_order = 0;
     // rows held at `lde` / `lde_next` (the debug build's bounds checks; 0 = not given)
     uint64_t lde_rows = 0, lde_next_rows = 0;
+    // alpha-independent evaluation (prove.cpp, "constraints before alpha"): with
+    // `cons` set, launch_quotient writes every constraint's value at each point
+    // (ncons of them, in eval's order) as limb-planar 29-bit words, thread t's
+    // value j limb l at cons[(j * 9 + l) * n + t], and folds nothing;
+    // launch_quotient_fold then folds them with `alpha` and 1/Z_H into `out`
+    uint32_t* cons = nullptr;
+    uint32_t ncons = 0;
 };
 // den[m] = (x_i - 1)(x_i - w_h^-1), x_i = GEN * w_Q^i, i = i0 + (m << log_step), m < n
 hipError_t launch_selector_denoms(const Fr* tabQ, uint32_t L1, Fr gen, Fr wh_inv, size_t n, Fr* den,
                                   hipStream_t st, uint64_t i0 = 0, uint32_t log_step = 0);
 hipError_t launch_quotient(const QuotientArgs& a, hipStream_t st);
+// out[m] = (sum_j alpha^(ncons-1-j) C_j) / Z_H from the values launch_quotient
+// wrote into a.cons (same points, thread order and bounds as launch_quotient)
+hipError_t launch_quotient_fold(const QuotientArgs& a, hipStream_t st);
 
 // --------------------------------------------------------- k_open.hip
 // den[i] = z - GEN * w_N^bitrev(row0 + i) for i < n (two-level table of w_N)

@@ -549,7 +549,12 @@ static bool zerocopy_top() {
     return on;
 }
 
-Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, const FoldSpec* fold) {
+// levels above this many digests fill the chip; the ones below run one wave per
+// SIMD or fewer (per-level rates)
+constexpr size_t WIDE_LEVEL_STOP = (size_t)1 << 16;
+
+Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, const FoldSpec* fold,
+                 const std::function<void(hipEvent_t)>* side) {
     hipStream_t st = ctx->stream;
     using clk = std::chrono::steady_clock;
     const auto tt0 = clk::now();
@@ -573,6 +578,10 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
         host = (Fr*)ctx->hbuf(top_buf_name(ctx), (2 * height - 1 + height * w) * sizeof(Fr));
         Fr* rows = host + 2 * height - 1;
         LSP_HIP(hipMemcpyAsync(rows, m.ptr[0], height * w * sizeof(Fr), hipMemcpyDeviceToHost, st));
+        if (side) {  // nothing left on the GPU for this tree
+            LSP_HIP(hipEventRecord(ctx->ev_wide, st));
+            (*side)(ctx->ev_wide);
+        }
         LSP_HIP(hipStreamSynchronize(st));
         pool.parallel_for((height + 7) / 8, [&](size_t b) {
             ctx->p2.hash_range(rows, w, host, 8 * b, std::min(height, 8 * b + 8));
@@ -584,11 +593,24 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
             LSP_HIP(launch_hash_rows(m, height, layers, ctx->rc29_dev, ctx->p2.L, st));
         if (top == 0) {
             LSP_HIP(launch_merkle_tree(layers, height, ctx->rc29_dev, ctx->p2.L, st));
+            if (side) {
+                LSP_HIP(hipEventRecord(ctx->ev_wide, st));
+                (*side)(ctx->ev_wide);
+            }
             return d2h_fr(ctx, layers + 2 * height - 2);
         }
         // all but the last two GPU levels; an event; the last two (~120 us) and the download
         size_t off1 = 0, len1 = height;
-        LSP_HIP(launch_merkle_levels(layers, height, 4 * top, ctx->rc29_dev, ctx->p2.L, &off1, &len1, st));
+        if (side) {  // the wide levels, the side work's event, then the narrow ones
+            size_t offw = 0, lenw = height;
+            LSP_HIP(launch_merkle_levels(layers, height, std::max(4 * top, WIDE_LEVEL_STOP), ctx->rc29_dev, ctx->p2.L,
+                                         &offw, &lenw, st));
+            LSP_HIP(hipEventRecord(ctx->ev_wide, st));
+            LSP_HIP(launch_merkle_levels(layers + offw, lenw, 4 * top, ctx->rc29_dev, ctx->p2.L, &off1, &len1, st));
+            off1 += offw;
+        } else {
+            LSP_HIP(launch_merkle_levels(layers, height, 4 * top, ctx->rc29_dev, ctx->p2.L, &off1, &len1, st));
+        }
         if (!ctx->ev_near) {
             LSP_HIP(hipEventCreateWithFlags(&ctx->ev_near, hipEventDisableTiming));
             LSP_HIP(hipEventCreateWithFlags(&ctx->ev_top, hipEventDisableTiming));
@@ -621,6 +643,7 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
             LSP_HIP(hipMemcpyAsync(host, layers + off, len * sizeof(Fr), hipMemcpyDeviceToHost, st));
         }
         LSP_HIP(hipEventRecord(ctx->ev_top, st));
+        if (side) (*side)(ctx->ev_wide);
         t_launched = clk::now();
         // sleep through the wide levels, then spin (with the pool awake) for the last ones
         resolve_timings(ctx);  // the previous proof's phase events, meanwhile
@@ -833,27 +856,10 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             lde_device(ctx, d_trace, h, w, lb, shifts.data(), lde, k0, nk);
         const auto t_lde_issued = std::chrono::steady_clock::now();
         T.end("coset_lde_batch");
-        Fr* tlay = ctx->fbuf("t_tree", 2 * S - 1);
-        std::vector<std::vector<Fr>> ttop, qtop;
-        T.begin("merkle tree");
-        proof->troot = shard_root(ctx, comm, commit_device(ctx, one_mat(lde, (uint32_t)w), S, tlay), ttop,
-                                  "trace subtree roots");
-        T.end("merkle tree");
-        T.end("commit to trace data");
-
-        // U7: the instance, then the quotient challenge (TranscriptCfg switches)
-        const TranscriptCfg& TC = ctx->transcript;
-        Challenger ch(&ctx->p2, TC.mont_bits);
-        if (TC.log_degree) ch.observe(fr_from_u64(log_h));
-        ch.observe(proof->troot);
-        if (TC.public_values)
-            for (size_t i = 0; i < npub; ++i) ch.observe(pub[i]);
-        const Fr alpha = ch.sample();
-
-        // ---- quotient.  Point i reads LDE rows bitrev_Q(i) and bitrev_Q(i + q):
-        // the ranks holding the first Q rows (Gq of them) each own the points
+        // ---- quotient set-up (nothing here depends on alpha).  Point i reads LDE
+        // rows bitrev_Q(i) and bitrev_Q(i + q): the ranks holding the first Q rows
+        // (Gq of them) each own the points
         // i = bitrev(g) mod Gq, which are whole chunks j = i mod q (Gq <= q).
-        T.begin("compute quotient polynomial");
         const size_t Sq = std::min(S, Q), Gq = Q / Sq, cpr = q / Gq;
         const uint32_t logGq = log2_exact(Gq);
         uint32_t L1Q;
@@ -884,6 +890,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             }
         }
         std::vector<Fr> zh(q), izh(q);
+        QuotientArgs qa;  // alpha set once sampled
         if (row0 < Q) {
             const uint64_t i0 = host_bitrev(g, logGq);
             // 1/((x-1)(x-w_h^-1)) depends on the domain only: cached per shape in the context
@@ -914,7 +921,6 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             ctx->h2d_async("q_zh_h", dzh, zh.data(), 2 * q * sizeof(Fr));
             int32_t* dair = (int32_t*)ctx->buf("air", air.raw.size() * sizeof(int32_t));
             ctx->h2d_async("air_h", dair, air.raw.data(), air.raw.size() * sizeof(int32_t));
-            QuotientArgs qa;
             qa.lde = lde;
             qa.w = (uint32_t)w;
             qa.logQ = logQ;
@@ -923,7 +929,6 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             qa.air_len = (uint32_t)air.raw.size();
             qa.pub_alpha = pub[0];
             qa.pub_delta = pub[1];
-            qa.alpha = alpha;
             qa.gen = GEN;
             qa.wh_inv = wh_inv;
             qa.tabQ = tabQ;
@@ -940,7 +945,74 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             qa.row0_next = row0_next;
             qa.lde_rows = S;
             qa.lde_next_rows = lde_next ? S : 0;
-            LSP_HIP(launch_quotient(qa, st));
+        }
+
+        // Constraints before alpha (round 4): every constraint C_j at this rank's
+        // points depends on the trace LDE and the public values only; alpha enters
+        // as the fold sum_j alpha^(n-1-j) C_j (air/src/lib.rs:116-167 through the
+        // folder).  So the constraint values are evaluated on a low-priority side
+        // stream once the trace tree's wide levels are done, beside its narrow
+        // levels and the host's tree top, where most SIMDs idle; after alpha one
+        // short kernel folds them.  For shapes whose evaluation outgrows that window
+        // (ncons x points > 2^23: 2^20 rows and up at q = 4, the wide AIRs) the
+        // quotient stays one kernel after alpha.  LSP_QUOTIENT_EARLY=0 / 1: never /
+        // always (read per proof).
+        bool early = false;
+        const uint32_t ncons = (uint32_t)air.stats(ctx->public_degree).second;
+        if (row0 < Q && !sub && ncons > 0) {
+            const char* e = std::getenv("LSP_QUOTIENT_EARLY");
+            early = e && *e ? *e != '0' : (uint64_t)ncons * Sq <= (1ull << 23);
+        }
+        struct SideJoin {  // the main stream never runs ahead of side work it did not wait for
+            lsp_ctx* ctx;
+            bool on = false;
+            ~SideJoin() {
+                if (on) (void)hipStreamWaitEvent(ctx->stream, ctx->ev_side, 0);
+            }
+        } side_join{ctx};
+        std::function<void(hipEvent_t)> side_fn;
+        if (early) {
+            hipStream_t s2 = ctx->side();
+            qa.cons = (uint32_t*)ctx->buf("q_cons", (size_t)ncons * 9 * Sq * sizeof(uint32_t));
+            qa.ncons = ncons;
+            side_fn = [&, s2](hipEvent_t ev) {
+                LSP_HIP(hipStreamWaitEvent(s2, ev, 0));
+                LSP_HIP(launch_quotient(qa, s2));
+                LSP_HIP(hipEventRecord(ctx->ev_side, s2));
+                side_join.on = true;
+            };
+        }
+
+        Fr* tlay = ctx->fbuf("t_tree", 2 * S - 1);
+        std::vector<std::vector<Fr>> ttop, qtop;
+        T.begin("merkle tree");
+        proof->troot = shard_root(ctx, comm,
+                                  commit_device(ctx, one_mat(lde, (uint32_t)w), S, tlay, nullptr, early ? &side_fn : nullptr),
+                                  ttop, "trace subtree roots");
+        T.end("merkle tree");
+        T.end("commit to trace data");
+
+        // U7: the instance, then the quotient challenge (TranscriptCfg switches)
+        const TranscriptCfg& TC = ctx->transcript;
+        Challenger ch(&ctx->p2, TC.mont_bits);
+        if (TC.log_degree) ch.observe(fr_from_u64(log_h));
+        ch.observe(proof->troot);
+        if (TC.public_values)
+            for (size_t i = 0; i < npub; ++i) ch.observe(pub[i]);
+        const Fr alpha = ch.sample();
+
+        // ---- quotient: the constraint fold by alpha, divided by Z_H
+        T.begin("compute quotient polynomial");
+        if (row0 < Q) {
+            qa.alpha = alpha;
+            if (early) {
+                LSP_REQUIRE(side_join.on, LSP_E_STATE, "the constraint evaluation was not issued");
+                LSP_HIP(hipStreamWaitEvent(st, ctx->ev_side, 0));
+                side_join.on = false;
+                LSP_HIP(launch_quotient_fold(qa, st));
+            } else {
+                LSP_HIP(launch_quotient(qa, st));
+            }
         }
         if (G > 1) {
             // rank r < Gq holds chunks j = bitrev(r) + Gq c as an h x cpr matrix: one

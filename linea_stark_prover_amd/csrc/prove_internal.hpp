@@ -17,7 +17,13 @@ void coset_idft_device(lsp_ctx* ctx, const Fr* d_evals, size_t h, size_t w, cons
 // into the leaf kernel; m.ptr[0] receives the folded vector)
 // the pending phase events of the last proof -> ctx->timings (prove.cpp)
 void resolve_timings(lsp_ctx* ctx);
-Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, const FoldSpec* fold = nullptr);
+// side (optional): called once, after the tree's launches are issued and before
+// the host waits for them, with an event on the context's stream that follows
+// the leaves and the wide levels (every level of more than 2^15 digests): work
+// queued behind it on another stream fills the chip beside the narrow levels
+// and the host's tree top
+Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, const FoldSpec* fold = nullptr,
+                 const std::function<void(hipEvent_t)>* side = nullptr);
 lsp_proof* prove_device(lsp_ctx* ctx, const Fr* d_trace, size_t h, size_t w, const Air& air, const Fr* pub,
                         size_t npub);
 struct Comm;

@@ -126,8 +126,10 @@ def parse(argv=None):
     ap.add_argument("--shard-leg-warmup", type=int, default=1)
     ap.add_argument("--shard-comm", choices=["auto", "rccl", "gloo"], default="auto",
                     help="auto: RCCL when every rank has its own GPU, else gloo")
-    ap.add_argument("--shard-timeout", type=float, default=900.0,
-                    help="seconds before a rank's watchdog abandons the sharded leg")
+    ap.add_argument("--shard-timeout", type=float, default=240.0,
+                    help="seconds before a rank's watchdog abandons the sharded leg (the 2^24 and 2^26 legs "
+                         "take well under a minute on 8 GPUs; a hung first multi-rank RCCL run must still "
+                         "leave time for the main line inside a driver's bench budget)")
     ap.add_argument("--no-host-trace-leg", action="store_true")
     ap.add_argument("--batch-leg", default="22",
                     help="log_n list of the batch leg (BASELINE configs[4]: one independent 2^22 proof per "

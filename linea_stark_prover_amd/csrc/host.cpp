@@ -8,6 +8,10 @@
 #include <cstdlib>
 #include <cstring>
 
+#if defined(__linux__)
+#include <sched.h>
+#endif
+
 namespace lsp {
 
 Fr host_generator() { return fr_from_u64(22); }
@@ -382,10 +386,18 @@ hipStream_t lsp_ctx::side() {
 lsp::HostPool& lsp_ctx::host_pool() {
     if (!pool_) {
         // up to 16 threads (a 1-GPU box's CPU share), fewer when the launcher
-        // says several ranks share this host (torchrun's LOCAL_WORLD_SIZE)
+        // says several ranks share this host (torchrun's LOCAL_WORLD_SIZE).  The
+        // CPUs counted are this process's affinity set (hardware_concurrency()
+        // counts the whole machine: 256 on a box whose GPU share is 16), so ranks
+        // that share a restricted CPU set do not oversubscribe it with spinning pools
         unsigned ranks = 1;
         if (const char* e = std::getenv("LOCAL_WORLD_SIZE")) ranks = (unsigned)std::max(1L, std::strtol(e, nullptr, 10));
-        unsigned n = std::min(16u, std::max(1u, std::thread::hardware_concurrency() / ranks));
+        unsigned cpus = std::thread::hardware_concurrency();
+#if defined(__linux__)
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) cpus = (unsigned)CPU_COUNT(&set);
+#endif
+        unsigned n = std::min(16u, std::max(1u, cpus / ranks));
         if (const char* e = std::getenv("LSP_HOST_THREADS")) n = (unsigned)std::max(1L, std::strtol(e, nullptr, 10));
         pool_.reset(new lsp::HostPool(n - 1));
     }

@@ -1452,7 +1452,12 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             }
         }
         LSP_REQUIRE(ptrs.size() == mine.size() * E, LSP_E_STATE, "query opening layout mismatch");
-        std::vector<Fr> slots((size_t)nq * E, fr_zero());
+        // one rank: every query is this rank's, in order, so the gathered openings
+        // are already the all-ranks layout and the records read them in place
+        // (two host copies of ~E * nq elements fewer between proofs)
+        const bool in_place = G == 1;
+        std::vector<Fr> slots(in_place ? 0 : (size_t)nq * E, fr_zero());
+        const Fr* opened = nullptr;  // the openings of every query, (owner rank, query)-major
         if (!ptrs.empty()) {
             // the gather reads its pointer list from pinned host memory and writes the
             // openings into coherent pinned memory: no copy either side of the kernel
@@ -1473,11 +1478,19 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                 LSP_HIP(hipMemcpyAsync(got, dgot, ptrs.size() * sizeof(Fr), hipMemcpyDeviceToHost, st));
             }
             LSP_HIP(hipStreamSynchronize(st));
-            for (size_t k = 0; k < mine.size(); ++k)
-                std::copy(got + k * E, got + (k + 1) * E, slots.begin() + (size_t)mine[k] * E);
+            if (in_place)
+                opened = got;
+            else
+                for (size_t k = 0; k < mine.size(); ++k)
+                    std::copy(got + k * E, got + (k + 1) * E, slots.begin() + (size_t)mine[k] * E);
         }
         const auto q2 = std::chrono::steady_clock::now();
-        const std::vector<Fr> all = G > 1 ? comm.allgather_fr(ctx, slots.data(), slots.size(), "query openings") : slots;
+        std::vector<Fr> all;
+        if (!in_place) {
+            all = comm.allgather_fr(ctx, slots.data(), slots.size(), "query openings");
+            opened = all.data();
+        }
+        LSP_REQUIRE(opened || nq == 0, LSP_E_STATE, "query openings missing");
         auto top_path = [&](const std::vector<std::vector<Fr>>& top, size_t sub, std::vector<Fr>& out) {
             for (uint32_t i = 0; i + 1 < top.size(); ++i) out.push_back(top[i][(sub >> i) ^ 1]);
         };
@@ -1491,7 +1504,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         HostPool serial_pool(0);
         (qpool ? ctx->host_pool() : serial_pool).parallel_for(nq, [&](size_t qi) {
             const size_t idx = idxs[qi], o = idx >> logS;
-            const Fr* e = all.data() + (o * nq + qi) * E;
+            const Fr* e = opened + (o * nq + qi) * E;
             lsp_query& qq = proof->queries[qi];
             qq.sib.clear();
             qq.sib.reserve(nr);

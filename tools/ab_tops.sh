@@ -1,3 +1,6 @@
+#!/bin/bash
+# Same-box A/B of the host tree tops: ab/lib_prev.so against the in-tree library, alternating,
+# with LSP_TIME_TOPS=1 (per-tree host levels, query-phase parts) at 2^19.
 set -o pipefail
 for i in 1 2 3; do
   for lib in ab/lib_prev.so linea_stark_prover_amd/_lib/liblsp_hip.so; do

@@ -1,3 +1,6 @@
+#!/bin/bash
+# The FRI host tail's boundary (LSP_FRI_HOST_TAIL = 2048, 1024, 512, 4096 leaves): per-round
+# host times (LSP_TIME_TOPS=1) and the 2^19 prove time for each.
 set -o pipefail
 mkdir -p gpurun_out
 for t in 2048 1024 512 4096; do

@@ -27,14 +27,26 @@ def load(path):
     from linea_stark_prover_amd import _lib
     L = ctypes.CDLL(os.path.abspath(path), mode=os.RTLD_LOCAL | os.RTLD_NOW)
     for name, (res, args) in _lib._SIGS.items():
-        f = getattr(L, name)
+        f = getattr(L, name, None)  # an older build lacks the later entry points
+        if f is None:
+            continue
         f.restype = res
         f.argtypes = args
     return L
 
 
+class LspParamsR3(ctypes.Structure):
+    """lsp_params as round 3's library took it (no struct_size, no transcript
+    switches): --r3-abi lets a round-3 build race the current one"""
+    _fields_ = [("sbox_degree", ctypes.c_uint32), ("rounds_f", ctypes.c_uint32), ("rounds_p", ctypes.c_uint32),
+                ("round_constants", ctypes.c_void_p), ("log_blowup", ctypes.c_uint32),
+                ("log_final_poly_len", ctypes.c_uint32), ("num_queries", ctypes.c_uint32),
+                ("proof_of_work_bits", ctypes.c_uint32), ("public_degree", ctypes.c_int32),
+                ("internal_diag", ctypes.c_void_p), ("external_mds", ctypes.c_void_p)]
+
+
 class Side:
-    def __init__(self, path, log_n, ncols=3):
+    def __init__(self, path, log_n, ncols=3, r3_abi=False):
         import numpy as np
         from linea_stark_prover_amd import _lib
         from linea_stark_prover_amd.air import permutation_air
@@ -45,7 +57,10 @@ class Side:
         a, d, rc = cfg.seeded()
         self.rc = rc
         self.pub = np.ascontiguousarray(np.concatenate([a, d]))
-        p = _lib.LspParams(sbox_degree=cfg.sbox_degree, rounds_f=cfg.rounds_f, rounds_p=cfg.rounds_p,
+        P = LspParamsR3 if r3_abi else _lib.LspParams
+        if r3_abi:  # this side's own CDLL: its create takes the older struct
+            L.lsp_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(LspParamsR3), ctypes.POINTER(ctypes.c_void_p)]
+        p = P(sbox_degree=cfg.sbox_degree, rounds_f=cfg.rounds_f, rounds_p=cfg.rounds_p,
                            round_constants=rc.ctypes.data, log_blowup=cfg.log_blowup,
                            log_final_poly_len=cfg.log_final_poly_len, num_queries=cfg.num_queries,
                            proof_of_work_bits=cfg.proof_of_work_bits, public_degree=cfg.public_degree)
@@ -88,10 +103,11 @@ def main():
     ap.add_argument("--pairs", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--env-b", default=None, help="VAR=VAL[,VAR=VAL...] set around B's proofs only")
+    ap.add_argument("--r3-abi", default="", help="a, b or ab: that side is a round-3 build (its lsp_params)")
     ap.add_argument("--swap", action="store_true",
                     help="one library + --env-b: apply the switch to context B, then to context A, half the pairs each")
     args = ap.parse_args()
-    A, B = Side(args.a, args.log_n), Side(args.b, args.log_n)
+    A, B = Side(args.a, args.log_n, r3_abi="a" in args.r3_abi), Side(args.b, args.log_n, r3_abi="b" in args.r3_abi)
     envs = [kv.split("=", 1) for kv in args.env_b.split(",")] if args.env_b else []
     if envs:
         B.name += f" [{args.env_b}]"

@@ -1,5 +1,6 @@
 """Throughput of P independent 2^log_n proofs in flight on ONE GPU (P
-contexts = P HIP streams, one host thread each) vs one at a time."""
+contexts = P HIP streams, one host thread each) vs one at a time.
+    python tools/time_pipeline.py [log_n] [proofs per context] [P,P,...]"""
 import os, sys, threading, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -12,7 +13,7 @@ a, d, _ = cfg.seeded()
 pub = np.concatenate([a, d])
 air = permutation_air(3)
 tr = gen_permutation_trace(log_n, 3, a, d)
-for P in (1, 2, 3):
+for P in ([int(x) for x in sys.argv[3].split(',')] if len(sys.argv) > 3 else (1, 2, 3)):
     ctxs = [Context(cfg) for _ in range(P)]
     ptrs = []
     for c in ctxs:

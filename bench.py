@@ -107,9 +107,17 @@ def parse(argv=None):
     ap.add_argument("--cpu-log-n", type=int, default=None,
                     help="CPU-baseline size (rows = 2^cpu_log_n; default: the headline's --log-n, BASELINE.md's "
                          "2^19 input)")
-    ap.add_argument("--cpu-runs", type=int, default=3, help="CPU-baseline timed runs (median; after 1 warm-up)")
-    ap.add_argument("--cpu-small-log-n", type=int, default=16,
-                    help="an extra, smaller CPU sample reported beside the headline one (0 disables)")
+    ap.add_argument("--cpu-runs", type=int, default=3, help="CPU-baseline timed runs (median)")
+    ap.add_argument("--cpu-warmup", type=int, default=0,
+                    help="untimed CPU-baseline runs first (0: the C restatement has no JIT or cache to warm; each "
+                         "run allocates and faults in its own buffers)")
+    ap.add_argument("--cpu-small-log-n", type=int, default=0,
+                    help="an extra, smaller CPU sample reported beside the headline one (0, the default, disables: "
+                         "the headline-size sample is the baseline)")
+    ap.add_argument("--wide-leg", type=int, default=20,
+                    help="log2 rows of the wide_c3 leg (BASELINE configs[2], the synthetic wide AIR, W = 184); "
+                         "0 skips")
+    ap.add_argument("--wide-steps", type=int, default=3, help="timed proofs of the wide_c3 leg (median)")
     ap.add_argument("--shape-leg", default="6",
                     help="ncols of the extra 2^log_n leg in bench.log's shape (6+6 columns, w = 14, the "
                          "reference's only measured run, bench.log:18-20); 'none' to skip")
@@ -202,6 +210,11 @@ def main():
             batch = {"error": f"{type(e).__name__}: {e}"}
         if rank == 0:
             out["batch"] = batch
+    if world == 1 and args.wide_leg > 0 and args.air == "perm" and not args.shard:
+        try:
+            out["wide_c3"] = wide_leg(args, dist, ctx, args.wide_leg)
+        except Exception as e:  # the main line is still reported
+            out["wide_c3"] = {"error": f"{type(e).__name__}: {e}"}
     if world == 1 and args.shape_leg != "none" and args.air == "perm" and not args.shard:
         try:
             out["shape_bench_log"] = shape_leg(args, dist, ctx, int(args.shape_leg))
@@ -347,6 +360,7 @@ def main_leg(args, dist, ranks_seen):
             "phases_source": "one untimed proof after the timed steps; the timed steps time only "
                              + " and ".join(ROOFLINE_PHASES) + " (the roofline objects' ms)",
             "lib_src_sha16": LIB_SRC,
+            "host_threads": ctx.host_threads(),
             "roofline": {"bound": "hbm", "kernel": "coset_lde_batch (trace, w x 2^log_n -> 8x)",
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": lde_traffic(args.log_n, w),
@@ -361,8 +375,11 @@ def main_leg(args, dist, ranks_seen):
                                    "peak_basis": "1024 SIMDs x 64 lanes / 4 cycles per v_mad_u64_u32 x 2.4 GHz / "
                                                  "128 MADs per 8 x 32-bit Montgomery product",
                                    "impl_mad_floor": ntt_impl_floor(frmul_gps, peak)},
-                         "note": "VALU-bound: valu_issue = share of SIMD cycles issuing VALU in the NTT passes "
-                                 "(PMC SQ_ACTIVE_INST_VALU, profiles/*_valu_pmc.json); HBM frac is low by design",
+                         "limiter": "valu",
+                         "note": "bound/frac are against HBM, the roofline the metric names (NTT HBM GB/s); the "
+                                 "kernel itself is limited by the integer VALU, not HBM (limiter): valu_issue = share "
+                                 "of SIMD cycles issuing VALU in the NTT passes (PMC SQ_ACTIVE_INST_VALU, "
+                                 "profiles/*_valu_pmc.json), frmul_frac = its Fr products against the 128-MAD peak",
                          "algorithmic_bytes": lde_bytes, "ms": lde_ms},
             "roofline_valu": {"bound": "valu", "kernel": "trace Merkle tree (Poseidon2 leaf hash + levels)",
                               "achieved": valu_achieved, "unit": "M perm/s",
@@ -385,13 +402,18 @@ def main_leg(args, dist, ranks_seen):
                               "peak_source": peak["source"] if peak else "profiles/r02_rates.json missing",
                               "fr_mul_achieved_g_per_s": valu_achieved * FR_MUL_PER_PERM / 1e3,
                               "fr_mul_peak_g_per_s": peak["gfrmul_per_s"] if peak else None,
-                              "calibrated_register_resident_mperm_per_s": ctx.calibrate_poseidon2(),
+                              "register_resident_chain_mperm_per_s": ctx.calibrate_poseidon2(),
+                              "register_resident_chain_note": "k_calib_perm: dependent permutation chains in "
+                                                              "registers, a latency-bound probe and not a peak "
+                                                              "(the tree's leaf kernel outruns it)",
                               "valu_issue": valu_issue(["k_hash_rows1<11u, 1>", "k_merkle_level<11u, 1>"]),
                               "valu_issue_source": VALU_SRC.get("src"),
                               "perms": trace_perms, "fr_mul_per_perm": FR_MUL_PER_PERM, "ms": merkle_ms},
         }
         if table is not None:
             out.update(table)
+        if shard and world > 1:
+            out["exchange"] = ctx.exchange_plan(h, w)
         if world == 1 and not shard and args.inflight > 1:
             out["inflight"] = inflight(args, cfg, air, pub, trace, ctx, dtrace)
         if world == 1 and not shard and not args.no_host_trace_leg:
@@ -460,6 +482,57 @@ def batch_leg(args, dist, ctx, sizes):
         run["verified_ranks"] = nok
         runs.append(run)
     return {"runs": runs}
+
+
+def wide_leg(args, dist, ctx, log_n):
+    """BASELINE configs[2]: the synthetic wide AIR -- 4 LogUp
+    lookups (3-column A, two 3-column tables) + 8 permutation groups of 6+6,
+    W = 184, trace/src/lookup.rs:46-176 and air/src/lib.rs:57-114 -- standing in
+    for zkevm.bin (.MISSING_LARGE_BLOBS:1), at 2^log_n rows, trace resident in
+    HBM: one warm-up, then the median of --wide-steps proofs.  The trace is the
+    one tests/test_gpu_fullsize_oracle.py checks (lsp_gen_wide_trace, host);
+    what bounds the proof is read off phases_ms and the kernels' stamped VALU
+    issue (k_quotient: "quotient-eval bound" in BASELINE's words)."""
+    from linea_stark_prover_amd.prover import StarkConfig, gen_wide_trace
+    from linea_stark_prover_amd.replicas import timed_steps
+    import numpy as np
+    cfg = StarkConfig(seed=args.seed)
+    a, d, _ = cfg.seeded()
+    pub = np.concatenate([a, d])
+    t0 = time.perf_counter()
+    trace, air = gen_wide_trace(log_n, a, d, seed=args.seed)
+    gen_s = time.perf_counter() - t0
+    h, w = trace.shape[0], trace.shape[1]
+    dtrace = ctx.dev_alloc(trace.nbytes)
+    step_s = []
+    try:
+        ctx.h2d(dtrace, trace)
+        del trace
+        step = lambda: ctx.prove(dtrace, air, pub, h, w)  # noqa: E731
+        elapsed, proof = timed_steps(step, args.wide_steps, 1, dist, sync=ctx.synchronize, step_times=step_s)
+        ctx.set_phase_timing(True)  # the phase breakdown from one more, untimed proof
+        step()
+        phases = {k: round(v, 3) for k, v in ctx.last_timings()}
+        ctx.set_phase_timing(True, only=ROOFLINE_PHASES)
+        verified = bool(ctx.verify(proof, air, pub))
+    finally:
+        ctx.dev_free(dtrace)
+    q = 1 << air_log_q(air, cfg)
+    N = h << cfg.log_blowup
+    med = statistics.median(step_s)
+    leaf_perms = N * ((w + 1) // 2)  # the trace tree's leaves: ceil(w/2) permutations per LDE row
+    merkle_ms = phases.get("merkle tree")
+    out = {"workload": f"wide AIR (4 LogUp lookups + 8 permutation groups of 6+6), 2^{log_n} rows (w={w}, q={q})",
+           "stands_in_for": "BASELINE configs[2]: Linea zkEVM trace from zkevm.bin, 2^20 rows (absent: "
+                            ".MISSING_LARGE_BLOBS:1)",
+           "steps": args.wide_steps, "warmup": 1, "prove_time_median_s": med, "prove_time_s": elapsed / args.wide_steps,
+           "value": h / med, "unit": "trace-rows/s", "verified": verified, "phases_ms": phases,
+           "trace_gen_s_host": round(gen_s, 2),
+           "trace_tree_mperm_per_s": (leaf_perms + N - 1) / (merkle_ms * 1e-3) / 1e6 if merkle_ms else None,
+           "valu_issue_k_quotient": valu_issue(["k_quotient"], "_wide"),
+           "valu_issue_leaf_hash": valu_issue(["k_hash_rows"], "_wide"),
+           "valu_issue_source": VALU_SRC.get("_wide")}
+    return out
 
 
 def shape_leg(args, dist, ctx, ncols):
@@ -631,7 +704,7 @@ def shard_leg(args, dist, ctx, sizes):
         seen = ctx.comm_info()[1]  # after the attach's allgather/bcast self-test
     else:
         seen = 1
-    res = {"comm": comm, "n_ranks_seen": seen, "scaling": "strong", "runs": []}
+    res = {"comm": comm, "n_ranks_seen": seen, "scaling": "strong", "host_threads": ctx.host_threads(), "runs": []}
     for log_n in sizes:
         h = 1 << log_n
         dtrace = ctx.gen_permutation_trace_device(log_n, args.ncols, a, d, seed=args.seed)
@@ -651,6 +724,8 @@ def shard_leg(args, dist, ctx, sizes):
                            f"rank(s)", "proof_bytes": len(proof) if proof else 0}
         if table is not None:
             run.update(table)
+        if world > 1:  # the inverse-NTT exchange this proof chose, on the attach-time calibration
+            run["exchange"] = ctx.exchange_plan(h, w)
         if rank == 0:
             t = time.perf_counter()
             run["verified"] = bool(ctx.verify(proof, air, pub))
@@ -785,16 +860,17 @@ def impl_mads_per_perm():
     return (3 * 8 + 22) * (3 * ns + 2 * nm) if nm and ns else None
 
 
-def valu_issue(kernels):
+def valu_issue(kernels, kind=""):
     """Time-weighted VALU issue share of the named kernels from the committed
-    PMC passes (tools/pmc_valu.sh -> profiles/*_valu_pmc.json): SIMD cycles
-    with a VALU instruction issuing (SQ_ACTIVE_INST_VALU over all waves) /
-    (1024 SIMDs x kernel cycles).  Only a profile stamped with this library's
-    source hash counts (lib_src_sha16); else None, with the reason in
-    VALU_SRC."""
+    PMC passes (tools/pmc_stamp.sh -> profiles/*_valu_pmc{kind}.json; kind
+    "_wide": the wide-AIR proof's passes): SIMD cycles with a VALU instruction
+    issuing (SQ_ACTIVE_INST_VALU over all waves) / (1024 SIMDs x kernel
+    cycles).  Only a profile stamped with this library's source hash counts
+    (lib_src_sha16); else None, with the reason in VALU_SRC[kind or "src"]."""
     import glob
     d, src, stale = None, None, []
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu_pmc.json"))):
+    key = kind or "src"
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_valu_pmc{kind}.json"))):
         try:
             x = json.load(open(path))
         except (OSError, ValueError):
@@ -804,10 +880,10 @@ def valu_issue(kernels):
         else:
             stale.append(os.path.basename(path))
     if not d:
-        VALU_SRC["src"] = (f"null: no profiles/*_valu_pmc.json measured on this build (lib_src_sha16 {LIB_SRC}; "
-                           f"{len(stale)} older profile(s) skipped)")
+        VALU_SRC[key] = (f"null: no profiles/*_valu_pmc{kind}.json measured on this build (lib_src_sha16 {LIB_SRC}; "
+                         f"{len(stale)} older profile(s) skipped)")
         return None
-    VALU_SRC["src"] = src
+    VALU_SRC[key] = src
     ks = [v for k, v in d["kernels"].items() if any(k.startswith(p) for p in kernels)]
     ms = sum(v["ms"] for v in ks)
     return round(sum(v["valu_issue"] * v["ms"] for v in ks) / ms, 3) if ms else None
@@ -859,20 +935,20 @@ def cpu_share() -> int:
     return min(n, omp) if omp > 0 else n
 
 
-def _cpu_prove_times(cref, args, log_n, runs, threads):
-    """warm-up + `runs` timed full proofs of the C restatement at 2^log_n rows"""
+def _cpu_prove_times(cref, args, log_n, runs, threads, warmup=0):
+    """`warmup` untimed + `runs` timed full proofs of the C restatement at 2^log_n rows"""
     p = cref.setup(args.seed)
     tb, w = cref.gen_perm_trace(p, log_n, args.ncols, seed=args.seed)
     air = cref.perm_air(args.ncols)
     ts = []
-    for k in range(runs + 1):
+    for k in range(runs + warmup):
         t = time.perf_counter()
         cref.prove(p, tb, 1 << log_n, w, air, nthreads=threads)
         dt = time.perf_counter() - t
-        if k:  # run 0 is the warm-up
+        if k >= warmup:
             ts.append(dt)
         # progress on stderr: a 2^19 CPU proof takes tens of seconds
-        print(f"[cpu_baseline] 2^{log_n} {'warm-up' if not k else f'run {k}/{runs}'}: {dt:.2f} s",
+        print(f"[cpu_baseline] 2^{log_n} {'warm-up' if k < warmup else f'run {k - warmup + 1}/{runs}'}: {dt:.2f} s",
               file=sys.stderr, flush=True)
     return ts
 
@@ -889,18 +965,20 @@ def cpu_baseline(args):
     threads = cpu_share()
     log_n = args.cpu_log_n if args.cpu_log_n is not None else args.log_n
     runs = max(args.cpu_runs, 1)
-    ts = _cpu_prove_times(cref, args, log_n, runs, threads)
+    ts = _cpu_prove_times(cref, args, log_n, runs, threads, max(args.cpu_warmup, 0))
     dt = statistics.median(ts)
     try:
         nproc = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
     except (OSError, ValueError):
         nproc = None
     out = {"value": (1 << log_n) / dt, "unit": "trace-rows/s", "cores": threads, "kind": "port",
-           "seconds": dt, "seconds_runs": [round(x, 3) for x in ts], "warmup": 1, "log_n": log_n, "nproc": nproc,
+           "seconds": dt, "seconds_runs": [round(x, 3) for x in ts], "warmup": max(args.cpu_warmup, 0),
+           "log_n": log_n, "nproc": nproc,
            "machine_cpus": os.cpu_count(), "cpu_model": cpu_model(),
            "sample": f"oracle/lsp_oracle.c full prove of the headline workload: {args.ncols}x{args.ncols} "
                      f"permutation AIR at 2^{log_n} rows (same AIR, conventions and seed as the GPU line), "
-                     f"median of {len(ts)} runs after 1 warm-up, {threads} threads = this process's CPU share "
+                     f"median of {len(ts)} runs ({max(args.cpu_warmup, 0)} warm-up), {threads} threads = this "
+                     f"process's CPU share "
                      f"(affinity / OMP_NUM_THREADS)",
            "gpu_speedup": None}
     if args.cpu_small_log_n and args.cpu_small_log_n < log_n:

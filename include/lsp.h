@@ -327,8 +327,27 @@ int lsp_ctx_attach_loopback(lsp_ctx *ctx, int rank, int size);
  * hipMemGetInfo of its GPU */
 int lsp_ctx_mem_stats(lsp_ctx *ctx, size_t *pool_bytes, size_t *device_used, size_t *device_total);
 /* collective check of the attached communicator: an allgather and a
- * broadcast of known patterns (LSP_E_STATE on wrong data) */
+ * broadcast of known patterns (LSP_E_STATE on wrong data).  With more than one
+ * rank it then calibrates the exchange: the allgather bandwidth into one rank
+ * (a 4 MiB probe, then 256 MiB unless the first is below 20 GB/s) and this
+ * GPU's inverse-NTT rate, the minimum of each over the ranks.  The sharded
+ * proofs choose their inverse-NTT exchange on those numbers (SURVEY 8(e) step
+ * 1: split by columns + an allgather of the coefficients, or a redundant
+ * inverse on every rank; lsp_comm_exchange_plan) */
 int lsp_comm_selftest(lsp_ctx *ctx);
+/* the exchange plan a sharded proof of an h x w trace makes on ctx's
+ * communicator: the calibrated allgather_gbs / intt_gelem_s (0 when the
+ * communicator was never self-tested), the probe's size, split (1 = columns
+ * split + allgather, 0 = redundant inverse on every rank) and the model's two
+ * costs in ms.  Any output but split may be NULL.  LSP_SHARD_SPLIT_INTT=0/1
+ * in the environment forces the choice. */
+int lsp_comm_exchange_plan(lsp_ctx *ctx, size_t h, size_t w, double *allgather_gbs, double *intt_gelem_s,
+                           size_t *probe_bytes, int *split, double *allgather_ms, double *redundant_ms);
+/* threads of ctx's host pool (tree tops, FRI tail, query assembly): up to 16,
+ * from this process's CPU affinity set -- divided among LOCAL_WORLD_SIZE
+ * ranks only when that set is the machine's or holds >= 16 CPUs per rank
+ * (else it is taken as this rank's own slice); LSP_HOST_THREADS overrides */
+int lsp_ctx_host_threads(lsp_ctx *ctx, int *n);
 /* rank and size of the attached communicator (LSP_E_STATE if none) */
 int lsp_comm_info(lsp_ctx *ctx, int *rank, int *size);
 /* The collective schedule of the last lsp_prove_sharded on ctx, one entry

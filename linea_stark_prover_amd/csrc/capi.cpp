@@ -78,7 +78,7 @@ const Fr* dev_in(lsp_ctx* ctx, const lsp_fr* p, size_t n, int mem, const char* n
     if (mem == LSP_MEM_DEVICE) return reinterpret_cast<const Fr*>(p);
     LSP_REQUIRE(mem == LSP_MEM_HOST, LSP_E_ARG, "mem must be LSP_MEM_HOST or LSP_MEM_DEVICE");
     Fr* d = ctx->fbuf(name, n ? n : 1);
-    if (n) LSP_HIP(hipMemcpyAsync(d, p, n * sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
+    if (n) ctx->upload(d, p, n * sizeof(Fr));  // pinned-ring staging for large inputs (host.cpp)
     return d;
 }
 Fr* dev_out(lsp_ctx* ctx, lsp_fr* p, size_t n, int mem, const char* name) {
@@ -304,6 +304,7 @@ int lsp_ctx_destroy(lsp_ctx* ctx) {
         if (kv.second.p) (void)hipHostFree(kv.second.p);
     for (auto& kv : ctx->twiddles) (void)hipFree(kv.second);
     for (auto& kv : ctx->stage_ev) (void)hipEventDestroy(kv.second);
+    for (hipEvent_t e : ctx->ring_ev) (void)hipEventDestroy(e);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     for (auto& t : ctx->pending_timings) {
         (void)hipEventDestroy(std::get<1>(t));
@@ -983,6 +984,32 @@ int lsp_comm_selftest(lsp_ctx* ctx) {
         LSP_HIP(hipStreamSynchronize(ctx->stream));
         for (size_t i = 0; i < n; ++i)
             LSP_REQUIRE(got[i] == 2654435761u + (uint32_t)i, LSP_E_STATE, "communicator bcast returned wrong data");
+        calibrate_exchange(ctx, c);  // what the sharded proofs' inverse-NTT exchange is chosen on
+    });
+}
+
+int lsp_comm_exchange_plan(lsp_ctx* ctx, size_t h, size_t w, double* allgather_gbs, double* intt_gelem_s,
+                           size_t* probe_bytes, int* split, double* allgather_ms, double* redundant_ms) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && split, LSP_E_ARG, "null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        LSP_REQUIRE(ctx->comm, LSP_E_STATE, "no communicator attached");
+        const Comm& c = *ctx->comm;
+        const ExchangePlan p = exchange_plan(c, h, w);
+        if (allgather_gbs) *allgather_gbs = c.ag_gbs;
+        if (intt_gelem_s) *intt_gelem_s = c.intt_gelem_s;
+        if (probe_bytes) *probe_bytes = c.ag_probe_bytes;
+        *split = p.split ? 1 : 0;
+        if (allgather_ms) *allgather_ms = p.allgather_ms;
+        if (redundant_ms) *redundant_ms = p.redundant_ms;
+    });
+}
+
+int lsp_ctx_host_threads(lsp_ctx* ctx, int* n) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && n, LSP_E_ARG, "null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        *n = (int)ctx->host_pool().size();
     });
 }
 

@@ -44,6 +44,13 @@ struct Comm {
     int rank = 0, size = 1;
     double init_ms = 0;          // communicator creation (RCCL: ncclCommInitRank), wall ms
     std::vector<CommRec> log;    // the collectives since the last begin_log()
+    // Exchange calibration (lsp_comm_selftest, calibrate_exchange in prove.cpp),
+    // the minimum over the ranks so every rank plans the same collectives:
+    // allgather bandwidth into one rank ((G - 1) shares / wall time, GB/s), the
+    // inverse NTT's rate on this GPU (G elements/s), and the probe's size.
+    // 0 = not measured (then the split inverse is the default).
+    double ag_gbs = 0, intt_gelem_s = 0;
+    size_t ag_probe_bytes = 0;
     virtual ~Comm() {
         for (CommRec& r : log) {
             if (r.e0) (void)hipEventDestroy(r.e0);

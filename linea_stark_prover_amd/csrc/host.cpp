@@ -372,6 +372,55 @@ void lsp_ctx::h2d_async(const std::string& name, void* dst, const void* src, siz
     LSP_HIP(hipEventRecord(it->second, stream));
 }
 
+// A large host -> device upload (the trace a drop-in prove receives in host
+// memory, bin/src/main.rs:72,80-86) through a ring of pinned slots: the host
+// pool's threads copy slot j while the DMA engine moves the slots before it.
+// A pageable hipMemcpyAsync stages through the runtime's own pinned buffers
+// with one thread and blocks until the last byte has left; here the caller's
+// buffer is free once the last slot is copied, and the DMAs run on ctx's
+// stream.  tools/ubench/h2d.hip measures the alternatives (pageable, pinned,
+// hipHostRegister per call, this ring).  LSP_H2D_STAGED=0: the pageable copy.
+void lsp_ctx::upload(void* dst, const void* src, size_t bytes) {
+    static const size_t chunk = [] {
+        const char* e = std::getenv("LSP_H2D_CHUNK_MB");
+        const long mb = e ? std::strtol(e, nullptr, 10) : 8;
+        return (size_t)std::max(1L, std::min(mb, 256L)) << 20;
+    }();
+    static const bool staged = [] {
+        const char* e = std::getenv("LSP_H2D_STAGED");
+        return !(e && *e == '0');
+    }();
+    constexpr int K = 4;  // slots in flight
+    if (!staged || bytes < 2 * chunk) {
+        LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+        return;
+    }
+    if (ring_ev.empty()) {
+        ring_ev.resize(K);
+        for (auto& e : ring_ev) LSP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    char* ring = (char*)hbuf("h2d_ring", K * chunk);
+    lsp::HostPool& P = host_pool();
+    const size_t T = P.size();
+    const size_t nch = (bytes + chunk - 1) / chunk;
+    P.wake();
+    for (size_t j = 0; j < nch; ++j) {
+        const int s = (int)(j % K);
+        if (ring_used[s]) LSP_HIP(hipEventSynchronize(ring_ev[s]));  // the slot's previous DMA has left
+        const size_t off = j * chunk, n = std::min(chunk, bytes - off);
+        char* slot = ring + (size_t)s * chunk;
+        const char* from = (const char*)src + off;
+        const size_t piece = ((n + T - 1) / T + 4095) & ~(size_t)4095;
+        P.parallel_for((n + piece - 1) / piece, [&](size_t t) {
+            const size_t o = t * piece;
+            std::memcpy(slot + o, from + o, std::min(piece, n - o));
+        });
+        LSP_HIP(hipMemcpyAsync((char*)dst + off, slot, n, hipMemcpyHostToDevice, stream));
+        LSP_HIP(hipEventRecord(ring_ev[s], stream));
+        ring_used[s] = true;
+    }
+}
+
 hipStream_t lsp_ctx::side() {
     if (!side_stream) {
         int least = 0, greatest = 0;
@@ -385,23 +434,32 @@ hipStream_t lsp_ctx::side() {
 
 lsp::HostPool& lsp_ctx::host_pool() {
     if (!pool_) {
-        // up to 16 threads (a 1-GPU box's CPU share), fewer when the launcher
-        // says several ranks share this host (torchrun's LOCAL_WORLD_SIZE).  The
-        // CPUs counted are this process's affinity set (hardware_concurrency()
-        // counts the whole machine: 256 on a box whose GPU share is 16), so ranks
-        // that share a restricted CPU set do not oversubscribe it with spinning pools
-        unsigned ranks = 1;
-        if (const char* e = std::getenv("LOCAL_WORLD_SIZE")) ranks = (unsigned)std::max(1L, std::strtol(e, nullptr, 10));
-        unsigned cpus = std::thread::hardware_concurrency();
-#if defined(__linux__)
-        cpu_set_t set;
-        if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) cpus = (unsigned)CPU_COUNT(&set);
-#endif
-        unsigned n = std::min(16u, std::max(1u, cpus / ranks));
-        if (const char* e = std::getenv("LSP_HOST_THREADS")) n = (unsigned)std::max(1L, std::strtol(e, nullptr, 10));
-        pool_.reset(new lsp::HostPool(n - 1));
+        pool_.reset(new lsp::HostPool(lsp::default_host_threads() - 1));
     }
     return *pool_;
+}
+
+// The host pool's size: up to 16 threads (a 1-GPU box's CPU share).  The CPUs
+// counted are this process's affinity set (hardware_concurrency() counts the
+// whole machine: 256 on a box whose GPU share is 16).  When the launcher says
+// several ranks share this host (torchrun's LOCAL_WORLD_SIZE), the set is
+// divided among them only if it is the shared one -- the whole machine, or at
+// least 16 CPUs per rank; a smaller set is taken as this rank's own slice
+// (a launcher that pins each rank, e.g. --cpu-bind or numactl per rank), which
+// dividing again would shrink to a few threads.  LSP_HOST_THREADS overrides.
+unsigned lsp::default_host_threads() {
+    unsigned ranks = 1;
+    if (const char* e = std::getenv("LOCAL_WORLD_SIZE")) ranks = (unsigned)std::max(1L, std::strtol(e, nullptr, 10));
+    const unsigned machine = std::max(1u, std::thread::hardware_concurrency());
+    unsigned cpus = machine;
+#if defined(__linux__)
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) cpus = (unsigned)CPU_COUNT(&set);
+#endif
+    const bool shared = cpus >= machine || cpus >= ranks * 16u;
+    unsigned n = std::min(16u, std::max(1u, shared ? cpus / ranks : cpus));
+    if (const char* e = std::getenv("LSP_HOST_THREADS")) n = (unsigned)std::max(1L, std::strtol(e, nullptr, 10));
+    return n;
 }
 
 const uint4* lsp_ctx::twiddle29(uint32_t logH, bool inverse) {

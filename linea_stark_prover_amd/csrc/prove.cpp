@@ -319,16 +319,91 @@ static void subcoset_lde(lsp_ctx* ctx, const Fr* coef, ColMap map, size_t h, siz
     lde_coeffs_device(ctx, folded, ColMap::plain((uint32_t)w), S, w, b, shifts_host, d_out, blk, 1);
 }
 
-// A sharded proof splits the inverse NTTs by columns (rank g inverts the
-// columns bitrev(g) + G k and the coefficients are exchanged) instead of every
-// rank inverting every column; LSP_SHARD_SPLIT_INTT=0 restores the redundant
-// per-rank inverse (A/B)
-static bool split_intt() {
-    static const bool on = [] {
+// A sharded proof either splits the inverse NTTs by columns (rank g inverts
+// the columns bitrev(g) + G k and the coefficients are allgathered) or has
+// every rank invert every column.  The split moves (G - 1) h ceil(w/G) elements
+// into every rank and saves (w - ceil(w/G)) h elements of inverse NTT; with
+// the communicator calibrated (lsp_comm_selftest) the cheaper one is taken --
+// on the same measured numbers on every rank, so the collective schedule
+// stays rank-identical.  Uncalibrated (in-process groups, a transport never
+// self-tested): the split.  LSP_SHARD_SPLIT_INTT=0/1 forces either (A/B).
+ExchangePlan exchange_plan(const Comm& comm, size_t h, size_t w) {
+    static const int forced = [] {
         const char* e = std::getenv("LSP_SHARD_SPLIT_INTT");
-        return !(e && *e == '0');
+        return e && *e ? (*e == '0' ? 0 : 1) : -1;
     }();
-    return on;
+    ExchangePlan p{true, 0, 0, "uncalibrated: split"};
+    const size_t G = (size_t)comm.size, cg = (w + G - 1) / G;
+    if (comm.ag_gbs > 0 && comm.intt_gelem_s > 0) {
+        p.allgather_ms = (double)((G - 1) * h * cg * sizeof(Fr)) / (comm.ag_gbs * 1e9) * 1e3;
+        p.redundant_ms = (double)((w - std::min(w, cg)) * h) / (comm.intt_gelem_s * 1e9) * 1e3;
+        p.split = p.allgather_ms < p.redundant_ms;
+        p.reason = p.split ? "measured: allgather cheaper than the redundant inverse"
+                           : "measured: redundant inverse cheaper than the allgather";
+    }
+    if (forced >= 0) {
+        p.split = forced == 1;
+        p.reason = "forced (LSP_SHARD_SPLIT_INTT)";
+    }
+    if (G == 1) p.split = false;
+    return p;
+}
+
+void calibrate_exchange(lsp_ctx* ctx, Comm& comm) {
+    if (comm.size < 2 || comm.rehearsal()) return;
+    hipStream_t st = ctx->stream;
+    const size_t G = (size_t)comm.size;
+    auto timed = [&](const std::function<void()>& f, int reps) {  // median wall ms of reps runs after a warm-up
+        std::vector<double> t;
+        for (int r = 0; r <= reps; ++r) {
+            LSP_HIP(hipStreamSynchronize(st));
+            const auto t0 = std::chrono::steady_clock::now();
+            f();
+            LSP_HIP(hipStreamSynchronize(st));
+            if (r) t.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        }
+        std::sort(t.begin(), t.end());
+        return t[t.size() / 2];
+    };
+    // the allgather: a 4 MiB probe first; only a transport that is not clearly
+    // below the break-even region (>= 20 GB/s) gets the 256 MiB one
+    auto probe = [&](size_t total) {
+        const size_t share = std::max<size_t>(total / G / 256, 1) * 256;
+        char* s = (char*)ctx->buf("calib_s", share);
+        char* r = (char*)ctx->buf("calib_r", share * G);
+        LSP_HIP(hipMemsetAsync(s, comm.rank & 0xff, share, st));
+        const double ms = timed([&] { comm.allgather(ctx, s, r, share, "calibration"); }, 3);
+        comm.ag_probe_bytes = share * G;
+        return (double)((G - 1) * share) / (ms * 1e-3) / 1e9;
+    };
+    double gbs = probe((size_t)4 << 20);
+    if (gbs >= 20) gbs = probe((size_t)256 << 20);
+    // the inverse NTT the split distributes: 8 columns of 2^20 (3 passes like the proofs' sizes)
+    const uint32_t logh = 20;
+    const size_t h = (size_t)1 << logh, w = 8;
+    Fr* x = ctx->fbuf("calib_x", h * w);
+    Fr* y = ctx->fbuf("calib_y", h * w);
+    LSP_HIP(hipMemsetAsync(x, 0, h * w * sizeof(Fr), st));
+    const uint4* tw = ctx->twiddle29(logh, true);
+    const double ms =
+        timed([&] { LSP_HIP(launch_intt(x, ColMap::plain((uint32_t)w), y, w, logh, tw, st)); }, 3);
+    const double rate = (double)(h * w) / (ms * 1e-3) / 1e9;
+    // agree on the minimum over the ranks (every rank then plans the same exchange)
+    double mine[2] = {gbs, rate};
+    double* ds = (double*)ctx->buf("calib_ds", sizeof mine);
+    double* dr = (double*)ctx->buf("calib_dr", sizeof mine * G);
+    LSP_HIP(hipMemcpyAsync(ds, mine, sizeof mine, hipMemcpyHostToDevice, st));
+    comm.allgather(ctx, ds, dr, sizeof mine, "calibration");
+    std::vector<double> all(2 * G);
+    LSP_HIP(hipMemcpyAsync(all.data(), dr, all.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+    LSP_HIP(hipStreamSynchronize(st));
+    comm.ag_gbs = all[0];
+    comm.intt_gelem_s = all[1];
+    for (size_t r = 1; r < G; ++r) {
+        comm.ag_gbs = std::min(comm.ag_gbs, all[2 * r]);
+        comm.intt_gelem_s = std::min(comm.intt_gelem_s, all[2 * r + 1]);
+    }
+    ctx->release("calib_");
 }
 
 // ------------------------------------------------------------- Merkle
@@ -825,7 +900,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         std::vector<Fr> shifts(std::max(w, q), GEN);
         T.begin("coset_lde_batch");
         span("coset_lde_batch", w, h, (int)lb);
-        const bool split = G > 1 && split_intt();
+        const bool split = G > 1 && exchange_plan(comm, h, w).split;
         const Fr* tcoef = nullptr;  // h * coefficients of the trace (split or sub), read through tmap
         ColMap tmap;
         if (split) {

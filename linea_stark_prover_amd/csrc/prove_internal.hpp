@@ -31,6 +31,19 @@ struct Comm;
 // every rank returns the same proof
 lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, size_t w, const Air& air,
                        const Fr* pub, size_t npub);
+// collective (every rank of comm): time an allgather of up to 256 MiB and this
+// GPU's inverse NTT, agree on the minimum over the ranks (comm.ag_gbs,
+// comm.intt_gelem_s)
+void calibrate_exchange(lsp_ctx* ctx, Comm& comm);
+// the inverse-NTT exchange a sharded proof of h x w over comm makes: true =
+// split by columns + an allgather of the coefficients, false = every rank
+// inverts every column (LSP_SHARD_SPLIT_INTT=0/1 forces it); rank-identical
+struct ExchangePlan {
+    bool split;
+    double allgather_ms, redundant_ms;  // the model's two costs (0 when uncalibrated)
+    const char* reason;
+};
+ExchangePlan exchange_plan(const Comm& comm, size_t h, size_t w);
 // proof wire format and field view (proof.cpp)
 // pool (optional): the queries are written in parallel (the element
 // conversions to canonical words are ~2/3 of a 2^19 proof's 10 K elements)

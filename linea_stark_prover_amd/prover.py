@@ -71,33 +71,24 @@ class StarkConfig:
         return a, d, rc
 
 
-# an uninitialised bytes object of a given size (CPython's C API), so the wire
-# bytes are written once, straight into the object the caller gets: no zero-filled
-# ctypes buffer and no copy out of it (~0.65 MB of memory traffic per 2^19 proof)
-_bytes_new = ctypes.pythonapi.PyBytes_FromStringAndSize
-_bytes_new.restype = ctypes.py_object
-_bytes_new.argtypes = (ctypes.c_char_p, ctypes.c_ssize_t)
-
-
 def _take_proof(proof: ctypes.c_void_p, size_only: bool = False):
     """serialize and free an lsp_proof handle (size_only: its wire size, the
-    one thing a rehearsal proof answers)"""
+    one thing a rehearsal proof answers).  The library writes into a bytearray
+    the caller's bytes are then copied from (one 324 KB copy per 2^19 proof,
+    tens of microseconds; round 4 wrote into an immutable bytes object instead)"""
     try:
         n = ctypes.c_size_t()
         L.check(L.lib().lsp_proof_serialize(proof, None, 0, ctypes.byref(n)))
         if size_only:
             return n.value
         size = n.value
-        if size < 2:  # CPython shares its empty and one-byte bytes objects: never write into those
-            buf = ctypes.create_string_buffer(max(size, 1))
-            L.check(L.lib().lsp_proof_serialize(proof, buf, size, ctypes.byref(n)))
-            return buf.raw[:n.value]
-        out = _bytes_new(None, size)  # fresh, referenced only here until it is returned
-        dst = ctypes.cast(ctypes.c_char_p(out), ctypes.c_void_p)  # its own buffer, not a copy
+        buf = bytearray(max(size, 1))
+        dst = (ctypes.c_char * len(buf)).from_buffer(buf)
         L.check(L.lib().lsp_proof_serialize(proof, dst, size, ctypes.byref(n)))
         if n.value != size:
             raise RuntimeError(f"lsp_proof_serialize wrote {n.value} of {size} bytes")
-        return out
+        del dst  # release the export before the copy
+        return bytes(buf[:size]) if size != len(buf) else bytes(buf)
     finally:
         L.lib().lsp_proof_free(proof)
 
@@ -341,6 +332,25 @@ class Context:
             self.dev_free(p)
             raise
         return p
+
+    def exchange_plan(self, h: int, w: int) -> dict:
+        """lsp_comm_exchange_plan: the calibrated allgather bandwidth and inverse-NTT
+        rate of the attached communicator and the inverse-NTT exchange a sharded
+        proof of h x w takes on them"""
+        gbs, rate, ms_ag, ms_red = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        probe, split = ctypes.c_size_t(), ctypes.c_int()
+        self._chk(L.lib().lsp_comm_exchange_plan(self.h, h, w, ctypes.byref(gbs), ctypes.byref(rate),
+                                                 ctypes.byref(probe), ctypes.byref(split), ctypes.byref(ms_ag),
+                                                 ctypes.byref(ms_red)))
+        return {"allgather_gbs": gbs.value, "intt_gelem_per_s": rate.value, "probe_bytes": probe.value,
+                "split_intt": bool(split.value), "model_allgather_ms": ms_ag.value,
+                "model_redundant_intt_ms": ms_red.value}
+
+    def host_threads(self) -> int:
+        """lsp_ctx_host_threads: the size of this context's host pool"""
+        n = ctypes.c_int()
+        self._chk(L.lib().lsp_ctx_host_threads(self.h, ctypes.byref(n)))
+        return n.value
 
     def comm_info(self) -> Tuple[int, int]:
         """(rank, size) of the attached communicator"""

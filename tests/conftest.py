@@ -29,6 +29,45 @@ def product_lib():
     return _lib.lib()
 
 
+@pytest.fixture
+def heartbeat(request):
+    """heartbeat(label): a context manager for a long silent stretch (an oracle
+    proof of minutes): every 30 s it prints a progress line past pytest's
+    capture and appends it to gpurun_out/heartbeat.log (on the GPU box), so a
+    runner that kills silent commands does not take it for a hang."""
+    import contextlib
+    import threading
+    import time
+
+    cap = request.config.pluginmanager.getplugin("capturemanager")
+    out_dir = os.path.join(ROOT, "gpurun_out") if os.environ.get("GRAFT_REPO_ROOT") else None
+
+    @contextlib.contextmanager
+    def run(label):
+        stop = threading.Event()
+        t0 = time.time()
+
+        def beat():
+            while not stop.wait(30):
+                line = f"[heartbeat] {request.node.name}: {label}, {time.time() - t0:.0f} s"
+                if cap is not None:
+                    with cap.global_and_fixture_disabled():
+                        print(line, file=sys.stderr, flush=True)
+                if out_dir:
+                    os.makedirs(out_dir, exist_ok=True)
+                    with open(os.path.join(out_dir, "heartbeat.log"), "a") as f:
+                        f.write(line + "\n")
+
+        th = threading.Thread(target=beat, daemon=True)
+        th.start()
+        try:
+            yield
+        finally:
+            stop.set()
+            th.join()
+    return run
+
+
 @pytest.fixture(scope="session")
 def gpu_ctx(product_lib):
     from linea_stark_prover_amd.prover import Context, StarkConfig

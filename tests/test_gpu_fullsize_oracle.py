@@ -1,0 +1,167 @@
+"""Whole-proof parity of BASELINE configs[1] and configs[2] at their full sizes,
+on the library under test (VERDICT r4 "next" #1).
+
+* configs[1]: the 3x3 permutation AIR at 2^22 rows.  The GPU proof of the
+  seeded trace (uploaded from host memory, as the reference's `prove` takes
+  it, bin/src/main.rs:72,80-86) byte for byte against the C oracle's proof of
+  the same trace (oracle/lsp_oracle.c; about 5 minutes on the box's 16-thread
+  CPU share).  Every size-dependent path of the library runs at this size:
+  the NTT pass plan of log h = 22 / 25, the early-quotient default, the FRI
+  host-tail threshold and the host tree tops.
+* configs[2]: the synthetic wide AIR (4 LogUp lookups + 8
+  permutation groups of 6+6, W = 184) at 2^20 rows.  The whole oracle proof
+  takes 12 minutes there (tools/full_oracle_proof.py w20, profiles/), so the
+  suite checks, at full size:
+    - the GPU proof is accepted by the oracle's own verifier (lo_verify, an
+      independent restatement of p3_uni_stark::verify);
+    - the opened values (A13) at zeta and zeta*w_h equal barycentric
+      evaluation of the trace columns (lo_eval_points: no NTT);
+    - lsp_quotient_values (A9/A10) over the device-resident 2^23 x 184 LDE at
+      320 sampled quotient points equals the Python oracle's
+      eval_constraints (air/src/lib.rs:57-167) folded with alpha and divided
+      by the vanishing polynomial, on LDE rows themselves checked against
+      barycentric evaluation;
+  with alpha and zeta replayed from the proof's own transcript (pyoracle
+  HashChallenger, U7 defaults).
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+THREADS = min(16, os.cpu_count() or 1)  # the GPU box's CPU share (os.cpu_count() shows the whole machine)
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+@pytest.mark.timeout(900)  # ~5 minutes of oracle proof; runners pass --timeout 120..300 per test
+def test_configs1_whole_proof_2e22_vs_oracle(gpu_ctx, oracle_lib, heartbeat):
+    from linea_stark_prover_amd.air import permutation_air
+    log_n = 22
+    p = oracle_lib.setup()
+    tb, w = oracle_lib.gen_perm_trace(p, log_n, 3)
+    trace = np.frombuffer(tb, dtype=np.uint64).reshape(1 << log_n, w, 4)
+    pub = np.concatenate([np.array(p.alpha, np.uint64).reshape(1, 4), np.array(p.delta, np.uint64).reshape(1, 4)])
+    proof = gpu_ctx.prove(trace, permutation_air(3), pub)
+    assert gpu_ctx.verify(proof, permutation_air(3), pub)
+    with heartbeat("C oracle proving 2^22 rows"):
+        expect = oracle_lib.prove(p, tb, 1 << log_n, w, oracle_lib.perm_air(3), nthreads=THREADS)
+    assert len(proof) == len(expect)
+    assert proof == expect
+
+
+def _replay(proof_bytes, pub_ints, perm):
+    """alpha and zeta of a serialized proof, from its roots (U7 defaults:
+    observe log h, trace root, public values; sample alpha; observe quotient
+    root; sample zeta)"""
+    pf = O.deserialize_proof(proof_bytes)
+    ch = O.HashChallenger(perm)
+    ch.observe(pf.degree_bits)
+    ch.observe(pf.trace_root)
+    ch.observe_slice(pub_ints)
+    alpha = ch.sample()
+    ch.observe(pf.quotient_root)
+    return pf, alpha, ch.sample()
+
+
+def _eval_points(L, trace, xs_int):
+    h, w = trace.shape[0], trace.shape[1]
+    from linea_stark_prover_amd.field import to_mont
+    xs = to_mont(xs_int)
+    out = np.zeros((len(xs_int), w, 4), np.uint64)
+    L.lo_eval_points(_p(trace), ctypes.c_size_t(h), ctypes.c_size_t(w), _p(xs), ctypes.c_size_t(len(xs_int)),
+                     _p(out), THREADS)
+    return out
+
+
+def test_configs2_wide_2e20_oracle_checks(gpu_ctx, oracle_lib):
+    from linea_stark_prover_amd import _lib
+    from linea_stark_prover_amd.field import from_mont, to_mont
+    from linea_stark_prover_amd.prover import gen_wide_trace
+    log_n, lb = 20, gpu_ctx.config.log_blowup
+    h = 1 << log_n
+    N = h << lb
+    a, d, _ = gpu_ctx.config.seeded()
+    trace, air = gen_wide_trace(log_n, a, d)
+    w = trace.shape[1]
+    assert w == 184
+    cfgs, _ = O.synthetic_wide_trace(2, 1, 2, O.DEFAULT_SEED)  # the same AIR layout (checked below)
+    assert oracle_lib.air_desc(cfgs) == list(air.descriptor())
+    pub = np.concatenate([a, d])
+    pub_ints = from_mont(pub)
+    s = O.setup_from_seed()
+    L = oracle_lib.lib()
+    p = oracle_lib.setup()
+
+    # ---- the proof: accepted by the oracle's verifier
+    proof = gpu_ctx.prove(trace, air, pub)
+    assert gpu_ctx.verify(proof, air, pub)
+    assert oracle_lib.verify(p, proof, list(air.descriptor())) == 0
+    pf, alpha, zeta = _replay(proof, pub_ints, s.perm)
+    assert pf.degree_bits == log_n and pf.width == w
+
+    # ---- opened values at zeta, zeta * w_h: barycentric, no NTT
+    zeta_next = zeta * O.two_adic_generator(log_n) % O.P
+    ys = from_mont(_eval_points(L, trace, [zeta, zeta_next]).reshape(-1, 4))
+    assert ys[:w] == pf.trace_local
+    assert ys[w:] == pf.trace_next
+
+    # ---- the quotient over the device-resident LDE at sampled points
+    log_q = pf.log_q
+    q, logQ = 1 << log_q, log_n + log_q
+    Q = 1 << logQ
+    row_b = w * 32
+    dtr = gpu_ctx.dev_alloc(trace.nbytes)
+    dlde = gpu_ctx.dev_alloc(N * row_b)
+    dq = gpu_ctx.dev_alloc(Q * 32)
+    try:
+        gpu_ctx.h2d(dtr, trace)
+        gen = to_mont([O.GENERATOR])
+        lib = _lib.lib()
+        gpu_ctx._chk(lib.lsp_coset_lde_batch(gpu_ctx.h, dtr, h, w, lb, _p(gen), dlde, _lib.LSP_MEM_DEVICE))
+        desc = (ctypes.c_int32 * len(air.descriptor()))(*air.descriptor())
+        al = to_mont([alpha])
+        gpu_ctx._chk(lib.lsp_quotient_values(gpu_ctx.h, dlde, h, w, desc, len(desc), _p(pub), 2, _p(al), dq,
+                                             _lib.LSP_MEM_DEVICE))
+        qv = np.zeros((Q, 4), np.uint64)
+        gpu_ctx.d2h(qv, dq)
+
+        def lde_row(j):
+            r = np.zeros((w, 4), np.uint64)
+            gpu_ctx.d2h(r, dlde + j * row_b)
+            return r
+
+        rng = np.random.default_rng(2020)
+        idx = sorted(set([0, 1, q - 1, q, Q - q, Q - 1] + [int(x) for x in rng.integers(0, Q, size=314)]))
+        assert len(idx) >= 256
+        # a few of those LDE rows against barycentric evaluation of the trace
+        chk = idx[:2] + idx[-2:]
+        xs = [O.GENERATOR * pow(O.two_adic_generator(logQ), i, O.P) % O.P for i in chk]
+        bary = _eval_points(L, trace, xs)
+        for k, i in enumerate(chk):
+            assert np.array_equal(lde_row(O.bitrev(i, logQ)), bary[k]), i
+        gq = O.two_adic_generator(logQ)
+        last = O.inv(O.two_adic_generator(log_n))
+        al_pub, de_pub = pub_ints
+        for i in idx:
+            local = from_mont(lde_row(O.bitrev(i, logQ)))   # get_evaluations_on_domain: natural order view
+            nxt = from_mont(lde_row(O.bitrev((i + q) % Q, logQ)))
+            x = O.GENERATOR * pow(gq, i, O.P) % O.P
+            z = (pow(x, h, O.P) - 1) % O.P
+            first_s = z * O.inv(x - 1) % O.P
+            last_s = z * O.inv(x - last) % O.P
+            cs = O.eval_constraints(cfgs, local, nxt, al_pub, de_pub, first_s, last_s, (x - last) % O.P)
+            acc = 0
+            for c in cs:
+                acc = (acc * alpha + c) % O.P
+            assert from_mont(qv[i:i + 1])[0] == acc * O.inv(z) % O.P, i
+    finally:
+        for ptr in (dq, dlde, dtr):
+            gpu_ctx.dev_free(ptr)

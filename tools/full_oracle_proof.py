@@ -18,12 +18,14 @@ import numpy as np  # noqa: E402
 
 from linea_stark_prover_amd.air import permutation_air  # noqa: E402
 from linea_stark_prover_amd.prover import Context, StarkConfig  # noqa: E402
+from linea_stark_prover_amd.build import library_hash, source_hash  # noqa: E402
 from oracle import cref  # noqa: E402
 
 nthreads = int(os.environ.get("LSP_ORACLE_THREADS", "16"))
 p = cref.setup()
 pub = np.concatenate([np.array(p.alpha, np.uint64).reshape(1, 4), np.array(p.delta, np.uint64).reshape(1, 4)])
 ok_all = True
+print(f"lib_src_sha16={library_hash() or source_hash()} (the library these GPU proofs come from)", flush=True)
 
 
 def heartbeat(stop):  # a line a minute while the oracle runs (long silent runs read as hung)

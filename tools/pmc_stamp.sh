@@ -8,6 +8,9 @@
 #   python tools/pmc_traffic.py gpurun_out/$TAG/fetch/lde_counter_collection.csv \
 #       gpurun_out/$TAG/write/lde_counter_collection.csv 524288 8 > profiles/${TAG}_lde_traffic.json
 #   python tools/pmc_valu_summary.py gpurun_out/$TAG/valu profiles/${TAG}_valu_pmc.json
+#   python tools/pmc_valu_summary.py gpurun_out/$TAG/valu_wide profiles/${TAG}_valu_pmc_wide.json
+# (the last: the same VALU group over one wide-AIR 2^20 prove, BASELINE configs[2],
+# which bench.py's wide_c3 leg reads)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -24,3 +27,6 @@ for grp in "SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_WAVES GRBM_GUI_ACTIVE" "SQ_ACTI
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/$TAG/valu/p$i -o run -- python3 tools/time_prove.py 19 > gpurun_out/$TAG.p$i.log 2>&1 || { tail -20 gpurun_out/$TAG.p$i.log; exit 1; }
 done
 echo "valu pmc done"
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT64 SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/$TAG/valu_wide/p1 -o run -- python3 tools/time_prove.py w20 > gpurun_out/$TAG.w1.log 2>&1 || { tail -20 gpurun_out/$TAG.w1.log; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES --output-format csv -d gpurun_out/$TAG/valu_wide/p2 -o run -- python3 tools/time_prove.py w20 > gpurun_out/$TAG.w2.log 2>&1 || { tail -20 gpurun_out/$TAG.w2.log; exit 1; }
+echo "wide valu pmc done"

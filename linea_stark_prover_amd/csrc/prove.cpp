@@ -328,10 +328,9 @@ static void subcoset_lde(lsp_ctx* ctx, const Fr* coef, ColMap map, size_t h, siz
 // stays rank-identical.  Uncalibrated (in-process groups, a transport never
 // self-tested): the split.  LSP_SHARD_SPLIT_INTT=0/1 forces either (A/B).
 ExchangePlan exchange_plan(const Comm& comm, size_t h, size_t w) {
-    static const int forced = [] {
-        const char* e = std::getenv("LSP_SHARD_SPLIT_INTT");
-        return e && *e ? (*e == '0' ? 0 : 1) : -1;
-    }();
+    // read per proof (not cached): tests flip it between proofs in one process
+    const char* fe = std::getenv("LSP_SHARD_SPLIT_INTT");
+    const int forced = fe && *fe ? (*fe == '0' ? 0 : 1) : -1;
     ExchangePlan p{true, 0, 0, "uncalibrated: split"};
     const size_t G = (size_t)comm.size, cg = (w + G - 1) / G;
     if (comm.ag_gbs > 0 && comm.intt_gelem_s > 0) {

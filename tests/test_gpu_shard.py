@@ -123,17 +123,27 @@ def test_group_rejects_too_many_ranks(gpu_ctx):
         grp.prove(tr, permutation_air(3), np.concatenate([a, d]))
 
 
-def test_group_large_equals_single(gpu_ctx):
-    """2^20 rows over 8 virtual ranks (default FRI slice threshold: sharded
-    rounds down to 8K-element slices, then replicated)"""
+@pytest.mark.parametrize("log_n,split", [(20, "1"), (22, "1"), (22, "0")])
+def test_group_large_equals_single(gpu_ctx, monkeypatch, log_n, split):
+    """2^20 and 2^22 (BASELINE configs[1]'s size) rows over 8 virtual ranks
+    (default FRI slice threshold: sharded rounds down to 8K-element slices,
+    then replicated), with the split inverse + coefficient allgather and with
+    the redundant inverse -- the two exchanges a calibrated communicator
+    chooses between (lsp_comm_exchange_plan)"""
     from linea_stark_prover_amd.air import permutation_air
     from linea_stark_prover_amd.prover import gen_permutation_trace
+    monkeypatch.setenv("LSP_SHARD_SPLIT_INTT", split)
     a, d, _ = gpu_ctx.config.seeded()
-    tr = gen_permutation_trace(20, 3, a, d)
+    tr = gen_permutation_trace(log_n, 3, a, d)
     pub = np.concatenate([a, d])
     single = gpu_ctx.prove(tr, permutation_air(3), pub)
-    grp, _ = _group(gpu_ctx, 8)
-    assert grp.prove(tr, permutation_air(3), pub) == single
+    grp, ctxs = _group(gpu_ctx, 8)
+    try:
+        assert grp.prove(tr, permutation_air(3), pub) == single
+    finally:
+        grp.close()
+        for c in ctxs:
+            c.close()
 
 
 @pytest.mark.parametrize("rank", [0, 7])

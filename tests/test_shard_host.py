@@ -118,3 +118,61 @@ def test_loopback_attach_and_mem_stats_checks(host_ctx):
     a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
     assert L.lib().lsp_ctx_mem_stats(host_ctx.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)) == L.LSP_E_STATE
     assert L.lib().lsp_ctx_detach_comm(host_ctx.h) == L.LSP_OK
+
+
+def test_exchange_plan_uncalibrated_and_forced(host_ctx, monkeypatch):
+    """lsp_comm_exchange_plan: a communicator never self-tested (here the
+    loopback rehearsal transport, which calibration skips) plans the split
+    inverse; LSP_SHARD_SPLIT_INTT forces either exchange, read per proof"""
+    from linea_stark_prover_amd import _lib
+    _lib.check(_lib.lib().lsp_ctx_attach_loopback(host_ctx.h, 0, 8), host_ctx.h)
+    p = host_ctx.exchange_plan(1 << 26, 8)
+    assert p["split_intt"] is True and p["allgather_gbs"] == 0 and p["model_allgather_ms"] == 0
+    monkeypatch.setenv("LSP_SHARD_SPLIT_INTT", "0")
+    assert host_ctx.exchange_plan(1 << 26, 8)["split_intt"] is False
+    monkeypatch.setenv("LSP_SHARD_SPLIT_INTT", "1")
+    assert host_ctx.exchange_plan(1 << 26, 8)["split_intt"] is True
+    _lib.check(_lib.lib().lsp_ctx_detach_comm(host_ctx.h), host_ctx.h)
+    with pytest.raises(_lib.LspError):
+        host_ctx.exchange_plan(1 << 20, 8)  # no communicator
+
+
+_POOL_CHILD = """
+import os, sys
+sys.path.insert(0, {root!r})
+cpus = {cpus!r}
+if cpus:
+    os.sched_setaffinity(0, set(sorted(os.sched_getaffinity(0))[:cpus]))
+from linea_stark_prover_amd.prover import Context, StarkConfig
+print(Context(StarkConfig(), device=-1).host_threads())
+"""
+
+
+def _shared(aff, ranks):  # host.cpp default_host_threads: the set is the shared one
+    return aff >= (os.cpu_count() or 1) or aff >= 16 * ranks
+
+
+@pytest.mark.parametrize("env,cpus,expect", [
+    ({"LSP_HOST_THREADS": "3"}, 0, lambda n: 3),
+    ({"LOCAL_WORLD_SIZE": "1"}, 0, lambda n: min(16, n)),
+    # the process's whole set (here the machine's) is shared by the local ranks: divided
+    ({"LOCAL_WORLD_SIZE": "4"}, 0, lambda n: max(1, min(16, n // 4 if _shared(n, 4) else n))),
+    # a 2-CPU slice smaller than the machine (and < 16 per rank) is this rank's own: not divided again
+    ({"LOCAL_WORLD_SIZE": "8"}, 2, lambda n: 2),
+])
+def test_host_pool_size(product_lib, env, cpus, expect):
+    """the host pool divides the CPU set among LOCAL_WORLD_SIZE ranks
+    only when the set is the shared one (the machine's, or >= 16 CPUs per rank);
+    a launcher that pins each rank to its own slice keeps that slice"""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    machine = len(os.sched_getaffinity(0))
+    if cpus and cpus >= machine:
+        pytest.skip("needs more CPUs than the slice")
+    e = {k: v for k, v in os.environ.items() if k not in ("LSP_HOST_THREADS", "LOCAL_WORLD_SIZE")}
+    e.update(env)
+    out = subprocess.run([sys.executable, "-c", _POOL_CHILD.format(root=root, cpus=cpus)], env=e,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert int(out.stdout.strip().splitlines()[-1]) == expect(machine)

@@ -17,6 +17,8 @@
 #   pmc              the PMC passes bench.py's roofline reads (tools/pmc_stamp.sh)
 #   rehearse         ranks 0, 5, 7 of the 2^26 proof over 8 ranks (tools/rank_rehearsal.py)
 #   py:<script>      python <script> under a 300 s limit (tools/ implied), output to a log
+#   h2d              tools/ubench/h2d: host -> device upload modes for a 128 MiB trace (build it first)
+#   tests900:<files> the listed test files with a 900 s per-test limit (the full-size oracle comparisons)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -77,6 +79,15 @@ import json
 for l in open('$log'):
     if l.startswith('{'):
         d = json.loads(l); print(d['rank'], round(d['prove_s_median'], 4), d['device_used_gib'], d['proof_wire_bytes'])" ;;
+    h2d)
+      timeout -k 10 120 tools/ubench/h2d 128 9 > gpurun_out/h2d_$TAG.json 2>&1 || fail "$step" gpurun_out/h2d_$TAG.json
+      cat gpurun_out/h2d_$TAG.json ;;
+    tests900:*)
+      log=gpurun_out/tests900_$TAG.log
+      files=$(echo "${step#tests900:}" | tr ',' '\n' | sed 's#^#tests/#' | tr '\n' ' ')
+      timeout -k 10 1100 python -u -m pytest -x -v --timeout 900 --timeout-method thread $files >> $log 2>&1 \
+        || fail "$step" $log
+      grep -E "passed|failed" $log | tail -1 ;;
     py:*)
       script=${step#py:}
       log=gpurun_out/$(basename ${script%% *} .py)_$TAG.log

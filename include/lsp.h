@@ -113,7 +113,13 @@ typedef struct {
      *                              check) takes the low bits of the Montgomery
      *                              form instead of the canonical value
      *   U12 skip_final_poly        1: the final polynomial's coefficients are
-     *                              not observed before grinding */
+     *                              not observed before grinding
+     * The switches are not recorded in the proof (the wire format, DESIGN.md
+     * §9, and p3_uni_stark::Proof<SC> have no field for them): prover and
+     * verifier must be configured alike.  A proof made under other conventions
+     * fails lsp_verify (and the reference's verify) with LSP_E_VERIFY at the
+     * first challenge-dependent check -- an opened value's Merkle path or the
+     * quotient identity at zeta -- and nothing in the bytes names the cause. */
     uint32_t skip_log_degree;
     uint32_t skip_public_values;
     uint32_t observe_opened_values;

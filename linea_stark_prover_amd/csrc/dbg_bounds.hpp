@@ -11,6 +11,15 @@
 // call and fails that call with LSP_E_STATE "device bounds check failed at
 // k_ntt.hip:123" (capi.cpp, bounds_fault_report).
 //
+// One fault word per translation unit for the whole process: the debug
+// library is meant for one context (one stream) at a time.  With several
+// contexts working at once (proofs in flight, the virtual ranks of an
+// lsp_prove_group) a failed check in one context's kernel may be read, cleared
+// and reported by another context's call, and the first call then returns
+// LSP_OK; the debug suites (tests/test_gpu_debug_bounds.py, the parity suites
+// under LSP_LIB=liblsp_hip_dbg.so) run one context at a time, and a group's
+// failure is still reported by one of its ranks.
+//
 // The checks compare indices derived from launch geometry (tile position,
 // row, column, LDS slot, table entry) with the extents the launch was planned
 // for, and value-derived indices (the reduction table's quotient digit) with

@@ -386,10 +386,8 @@ void lsp_ctx::upload(void* dst, const void* src, size_t bytes) {
         const long mb = e ? std::strtol(e, nullptr, 10) : 8;
         return (size_t)std::max(1L, std::min(mb, 256L)) << 20;
     }();
-    static const bool staged = [] {
-        const char* e = std::getenv("LSP_H2D_STAGED");
-        return !(e && *e == '0');
-    }();
+    const char* se = std::getenv("LSP_H2D_STAGED");  // per call: same-process A/B (tools/time_upload.py)
+    const bool staged = !(se && *se == '0');
     constexpr int K = 4;  // slots in flight
     if (!staged || bytes < 2 * chunk) {
         LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));

@@ -73,12 +73,14 @@ int guarded(lsp_ctx* ctx, F&& f) {
 }
 
 // device input: either the caller's device pointer or a pool copy of host data
-const Fr* dev_in(lsp_ctx* ctx, const lsp_fr* p, size_t n, int mem, const char* name) {
+// (pin: the caller's buffer is page-locked in place and the copy queued
+// asynchronously -- single-context calls that unpin_host() before returning)
+const Fr* dev_in(lsp_ctx* ctx, const lsp_fr* p, size_t n, int mem, const char* name, bool pin = false) {
     LSP_REQUIRE(p || n == 0, LSP_E_ARG, "null input pointer");
     if (mem == LSP_MEM_DEVICE) return reinterpret_cast<const Fr*>(p);
     LSP_REQUIRE(mem == LSP_MEM_HOST, LSP_E_ARG, "mem must be LSP_MEM_HOST or LSP_MEM_DEVICE");
     Fr* d = ctx->fbuf(name, n ? n : 1);
-    if (n) ctx->upload(d, p, n * sizeof(Fr));  // pinned-ring staging for large inputs (host.cpp)
+    if (n) ctx->upload(d, p, n * sizeof(Fr), pin);
     return d;
 }
 Fr* dev_out(lsp_ctx* ctx, lsp_fr* p, size_t n, int mem, const char* name) {
@@ -304,7 +306,7 @@ int lsp_ctx_destroy(lsp_ctx* ctx) {
         if (kv.second.p) (void)hipHostFree(kv.second.p);
     for (auto& kv : ctx->twiddles) (void)hipFree(kv.second);
     for (auto& kv : ctx->stage_ev) (void)hipEventDestroy(kv.second);
-    for (hipEvent_t e : ctx->ring_ev) (void)hipEventDestroy(e);
+    for (void* p : ctx->pinned_host) (void)hipHostUnregister(p);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     for (auto& t : ctx->pending_timings) {
         (void)hipEventDestroy(std::get<1>(t));
@@ -794,7 +796,16 @@ int lsp_prove(lsp_ctx* ctx, const lsp_fr* trace, size_t h, size_t w, const int32
         const Air A = Air::parse(air, air_len);
         std::vector<Fr> pub(npub);
         for (size_t i = 0; i < npub; ++i) pub[i] = to_fr(pubv[i]);
-        const Fr* din = dev_in(ctx, trace, h * w, mem, "trace_in");
+        const Fr* din = dev_in(ctx, trace, h * w, mem, "trace_in", true);
+        struct Unpin {  // every exit, the throwing ones too
+            lsp_ctx* c;
+            ~Unpin() {
+                try {
+                    c->unpin_host();
+                } catch (...) {
+                }
+            }
+        } unpin{ctx};
         *out = prove_device(ctx, din, h, w, A, pub.data(), npub);
     });
 }

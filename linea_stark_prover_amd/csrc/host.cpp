@@ -373,50 +373,43 @@ void lsp_ctx::h2d_async(const std::string& name, void* dst, const void* src, siz
 }
 
 // A large host -> device upload (the trace a drop-in prove receives in host
-// memory, bin/src/main.rs:72,80-86) through a ring of pinned slots: the host
-// pool's threads copy slot j while the DMA engine moves the slots before it.
-// A pageable hipMemcpyAsync stages through the runtime's own pinned buffers
-// with one thread and blocks until the last byte has left; here the caller's
-// buffer is free once the last slot is copied, and the DMAs run on ctx's
-// stream.  tools/ubench/h2d.hip measures the alternatives (pageable, pinned,
-// hipHostRegister per call, this ring).  LSP_H2D_STAGED=0: the pageable copy.
-void lsp_ctx::upload(void* dst, const void* src, size_t bytes) {
-    static const size_t chunk = [] {
-        const char* e = std::getenv("LSP_H2D_CHUNK_MB");
-        const long mb = e ? std::strtol(e, nullptr, 10) : 8;
-        return (size_t)std::max(1L, std::min(mb, 256L)) << 20;
-    }();
-    const char* se = std::getenv("LSP_H2D_STAGED");  // per call: same-process A/B (tools/time_upload.py)
-    const bool staged = !(se && *se == '0');
-    constexpr int K = 4;  // slots in flight
-    if (!staged || bytes < 2 * chunk) {
-        LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
-        return;
+// memory, bin/src/main.rs:72,80-86).  tools/ubench/h2d.hip measured the ways
+// to move a 128 MiB trace on the box (profiles/r05b_h2d.json): a pageable
+// hipMemcpyAsync 56.5 GB/s, from pinned memory 57.4, hipHostRegister of the
+// caller's buffer + copy + unregister 57.3, a ring of pinned slots filled by
+// host threads 37-43 -- PCIe, not the staging, is the limit.  The pageable
+// copy blocks the calling thread until the last byte has left, so the
+// proof's host-side set-up waits behind it; with `pin` the caller's buffer is
+// registered (page-locked in place, no copy) and the DMA is queued
+// asynchronously on the stream, so the host goes on issuing the proof while
+// the bytes move.  The registration is dropped at the next unpin_host()
+// (after the stream is drained; lsp_prove calls it before returning).
+// `pin` is only for single-context calls: ranks of a group may share one
+// host buffer, and one rank's unregister must not race another's DMA.
+// LSP_H2D_PIN=0 (read per call): the pageable copy (tools/time_upload.py).
+void lsp_ctx::upload(void* dst, const void* src, size_t bytes, bool pin) {
+    const char* pe = std::getenv("LSP_H2D_PIN");
+    if (pin && bytes >= ((size_t)4 << 20) && !(pe && *pe == '0')) {
+        const hipError_t e = hipHostRegister(const_cast<void*>(src), bytes, hipHostRegisterDefault);
+        if (e == hipSuccess) {
+            pinned_host.push_back(const_cast<void*>(src));
+            LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+            return;
+        }
+        (void)hipGetLastError();  // already registered (the caller's own pinned memory) or not registrable
+        if (e == hipErrorHostMemoryAlreadyRegistered) {
+            LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+            return;
+        }
     }
-    if (ring_ev.empty()) {
-        ring_ev.resize(K);
-        for (auto& e : ring_ev) LSP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    char* ring = (char*)hbuf("h2d_ring", K * chunk);
-    lsp::HostPool& P = host_pool();
-    const size_t T = P.size();
-    const size_t nch = (bytes + chunk - 1) / chunk;
-    P.wake();
-    for (size_t j = 0; j < nch; ++j) {
-        const int s = (int)(j % K);
-        if (ring_used[s]) LSP_HIP(hipEventSynchronize(ring_ev[s]));  // the slot's previous DMA has left
-        const size_t off = j * chunk, n = std::min(chunk, bytes - off);
-        char* slot = ring + (size_t)s * chunk;
-        const char* from = (const char*)src + off;
-        const size_t piece = ((n + T - 1) / T + 4095) & ~(size_t)4095;
-        P.parallel_for((n + piece - 1) / piece, [&](size_t t) {
-            const size_t o = t * piece;
-            std::memcpy(slot + o, from + o, std::min(piece, n - o));
-        });
-        LSP_HIP(hipMemcpyAsync((char*)dst + off, slot, n, hipMemcpyHostToDevice, stream));
-        LSP_HIP(hipEventRecord(ring_ev[s], stream));
-        ring_used[s] = true;
-    }
+    LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+}
+
+void lsp_ctx::unpin_host() {
+    if (pinned_host.empty()) return;
+    LSP_HIP(hipStreamSynchronize(stream));
+    for (void* p : pinned_host) (void)hipHostUnregister(p);
+    pinned_host.clear();
 }
 
 hipStream_t lsp_ctx::side() {

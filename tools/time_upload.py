@@ -1,8 +1,10 @@
 """Same-process A/B of the drop-in upload: one 2^19 proof
 with the trace resident in HBM against the same proof from pageable host
-memory, the upload through the pinned ring (LSP_H2D_STAGED=1, the default)
-and through one pageable hipMemcpyAsync (LSP_H2D_STAGED=0), interleaved
-round-robin so box drift hits every mode alike.
+memory -- the caller's buffer registered in place with the DMA queued
+asynchronously (LSP_H2D_PIN=1, the default), the same on a freshly allocated
+copy of the trace every step (what a caller handing over a new Vec pays:
+first-time page locking), and one synchronous pageable hipMemcpyAsync
+(LSP_H2D_PIN=0) -- interleaved round-robin so box drift hits every mode alike.
 Usage: time_upload.py [LOG_N] [ROUNDS]"""
 import os
 import statistics
@@ -32,18 +34,30 @@ def resident():
     return ctx.prove(dp, air, pub, h, w)
 
 
-def host(staged):
-    os.environ["LSP_H2D_STAGED"] = "1" if staged else "0"
-    return ctx.prove(tr, air, pub)
+def host(pin, t=None):
+    os.environ["LSP_H2D_PIN"] = "1" if pin else "0"
+    return ctx.prove(tr if t is None else t, air, pub)
 
 
-modes = {"resident": resident, "host_ring": lambda: host(True), "host_pageable": lambda: host(False)}
+fresh = [None]
+
+
+def host_fresh():
+    return host(True, fresh[0])
+
+
+modes = {"resident": resident, "host_pinned": lambda: host(True), "host_pinned_fresh": host_fresh,
+         "host_pageable": lambda: host(False)}
 ref = resident()
-for f in modes.values():  # warm every path (pinned ring allocation, pool threads)
+fresh[0] = tr.copy()
+for f in modes.values():  # warm every path
     assert f() == ref
 ts = {k: [] for k in modes}
 for r in range(rounds):
     for k, f in modes.items():
+        if k == "host_pinned_fresh":
+            fresh[0] = None
+            fresh[0] = tr.copy()  # new pages, written (outside the timed region)
         ctx.synchronize()
         t = time.perf_counter()
         f()
@@ -51,8 +65,7 @@ for r in range(rounds):
 med = {k: statistics.median(v) * 1e3 for k, v in ts.items()}
 print(f"log_n={log_n} trace {tr.nbytes / 2**20:.0f} MiB, {rounds} interleaved rounds, median ms: "
       + ", ".join(f"{k} {v:.2f}" for k, v in med.items()))
-print(f"host_ring - resident = {med['host_ring'] - med['resident']:.2f} ms; "
-      f"host_pageable - resident = {med['host_pageable'] - med['resident']:.2f} ms; "
-      f"upload rate through the ring {tr.nbytes / max(med['host_ring'] - med['resident'], 1e-3) / 1e6:.1f} GB/s "
-      f"(of the proof's added time)")
+for k in ("host_pinned", "host_pinned_fresh", "host_pageable"):
+    add = med[k] - med["resident"]
+    print(f"{k} - resident = {add:.2f} ms ({tr.nbytes / max(add, 1e-3) / 1e6:.1f} GB/s of the proof's added time)")
 ctx.dev_free(dp)

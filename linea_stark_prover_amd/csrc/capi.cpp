@@ -72,15 +72,19 @@ int guarded(lsp_ctx* ctx, F&& f) {
     }
 }
 
-// device input: either the caller's device pointer or a pool copy of host data
-// (pin: the caller's buffer is page-locked in place and the copy queued
-// asynchronously -- single-context calls that unpin_host() before returning)
-const Fr* dev_in(lsp_ctx* ctx, const lsp_fr* p, size_t n, int mem, const char* name, bool pin = false) {
+// device input: either the caller's device pointer or a pool copy of host data.
+// The host copy is one pageable hipMemcpyAsync: it moves a 2^19 x 8 trace at
+// 56 GB/s, the PCIe link's rate -- the same as from pinned memory (57) or from
+// the caller's buffer registered in place (57; 27 once the registration of a
+// fresh buffer is counted), and faster than staging through a pinned ring
+// filled by host threads (37-46): tools/ubench/h2d.hip, profiles/r05b_h2d.json,
+// r05c_h2d.json; in-proof A/B tools/time_upload.py, profiles/r05c_time_upload.txt
+const Fr* dev_in(lsp_ctx* ctx, const lsp_fr* p, size_t n, int mem, const char* name) {
     LSP_REQUIRE(p || n == 0, LSP_E_ARG, "null input pointer");
     if (mem == LSP_MEM_DEVICE) return reinterpret_cast<const Fr*>(p);
     LSP_REQUIRE(mem == LSP_MEM_HOST, LSP_E_ARG, "mem must be LSP_MEM_HOST or LSP_MEM_DEVICE");
     Fr* d = ctx->fbuf(name, n ? n : 1);
-    if (n) ctx->upload(d, p, n * sizeof(Fr), pin);
+    if (n) LSP_HIP(hipMemcpyAsync(d, p, n * sizeof(Fr), hipMemcpyHostToDevice, ctx->stream));
     return d;
 }
 Fr* dev_out(lsp_ctx* ctx, lsp_fr* p, size_t n, int mem, const char* name) {
@@ -306,7 +310,6 @@ int lsp_ctx_destroy(lsp_ctx* ctx) {
         if (kv.second.p) (void)hipHostFree(kv.second.p);
     for (auto& kv : ctx->twiddles) (void)hipFree(kv.second);
     for (auto& kv : ctx->stage_ev) (void)hipEventDestroy(kv.second);
-    for (void* p : ctx->pinned_host) (void)hipHostUnregister(p);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     for (auto& t : ctx->pending_timings) {
         (void)hipEventDestroy(std::get<1>(t));
@@ -796,16 +799,7 @@ int lsp_prove(lsp_ctx* ctx, const lsp_fr* trace, size_t h, size_t w, const int32
         const Air A = Air::parse(air, air_len);
         std::vector<Fr> pub(npub);
         for (size_t i = 0; i < npub; ++i) pub[i] = to_fr(pubv[i]);
-        const Fr* din = dev_in(ctx, trace, h * w, mem, "trace_in", true);
-        struct Unpin {  // every exit, the throwing ones too
-            lsp_ctx* c;
-            ~Unpin() {
-                try {
-                    c->unpin_host();
-                } catch (...) {
-                }
-            }
-        } unpin{ctx};
+        const Fr* din = dev_in(ctx, trace, h * w, mem, "trace_in");
         *out = prove_device(ctx, din, h, w, A, pub.data(), npub);
     });
 }

@@ -372,46 +372,6 @@ void lsp_ctx::h2d_async(const std::string& name, void* dst, const void* src, siz
     LSP_HIP(hipEventRecord(it->second, stream));
 }
 
-// A large host -> device upload (the trace a drop-in prove receives in host
-// memory, bin/src/main.rs:72,80-86).  tools/ubench/h2d.hip measured the ways
-// to move a 128 MiB trace on the box (profiles/r05b_h2d.json): a pageable
-// hipMemcpyAsync 56.5 GB/s, from pinned memory 57.4, hipHostRegister of the
-// caller's buffer + copy + unregister 57.3, a ring of pinned slots filled by
-// host threads 37-43 -- PCIe, not the staging, is the limit.  The pageable
-// copy blocks the calling thread until the last byte has left, so the
-// proof's host-side set-up waits behind it; with `pin` the caller's buffer is
-// registered (page-locked in place, no copy) and the DMA is queued
-// asynchronously on the stream, so the host goes on issuing the proof while
-// the bytes move.  The registration is dropped at the next unpin_host()
-// (after the stream is drained; lsp_prove calls it before returning).
-// `pin` is only for single-context calls: ranks of a group may share one
-// host buffer, and one rank's unregister must not race another's DMA.
-// LSP_H2D_PIN=0 (read per call): the pageable copy (tools/time_upload.py).
-void lsp_ctx::upload(void* dst, const void* src, size_t bytes, bool pin) {
-    const char* pe = std::getenv("LSP_H2D_PIN");
-    if (pin && bytes >= ((size_t)4 << 20) && !(pe && *pe == '0')) {
-        const hipError_t e = hipHostRegister(const_cast<void*>(src), bytes, hipHostRegisterDefault);
-        if (e == hipSuccess) {
-            pinned_host.push_back(const_cast<void*>(src));
-            LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
-            return;
-        }
-        (void)hipGetLastError();  // already registered (the caller's own pinned memory) or not registrable
-        if (e == hipErrorHostMemoryAlreadyRegistered) {
-            LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
-            return;
-        }
-    }
-    LSP_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
-}
-
-void lsp_ctx::unpin_host() {
-    if (pinned_host.empty()) return;
-    LSP_HIP(hipStreamSynchronize(stream));
-    for (void* p : pinned_host) (void)hipHostUnregister(p);
-    pinned_host.clear();
-}
-
 hipStream_t lsp_ctx::side() {
     if (!side_stream) {
         int least = 0, greatest = 0;

@@ -352,12 +352,6 @@ struct lsp_ctx {
     // buffer `name`: the caller's memory may be reused at return and the
     // stream is not drained (only the previous copy out of `name` is awaited)
     void h2d_async(const std::string& name, void* dst, const void* src, size_t bytes);
-    // a host -> device copy on `stream`; pin: register the caller's buffer and
-    // queue the DMA asynchronously (host.cpp) -- the buffer must then stay valid
-    // until unpin_host(), which drains the stream and drops the registrations
-    void upload(void* dst, const void* src, size_t bytes, bool pin = false);
-    void unpin_host();
-    std::vector<void*> pinned_host;  // caller buffers registered by upload(pin)
     // w_H^x (or its inverse) for x < H/2, in the 29-bit Montgomery form the NTT multiplies by (k_ntt.hip)
     const uint4* twiddle29(uint32_t logH, bool inverse);
     lsp::HostPool& host_pool();

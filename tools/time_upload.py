@@ -1,10 +1,11 @@
-"""Same-process A/B of the drop-in upload: one 2^19 proof
-with the trace resident in HBM against the same proof from pageable host
-memory -- the caller's buffer registered in place with the DMA queued
-asynchronously (LSP_H2D_PIN=1, the default), the same on a freshly allocated
-copy of the trace every step (what a caller handing over a new Vec pays:
-first-time page locking), and one synchronous pageable hipMemcpyAsync
-(LSP_H2D_PIN=0) -- interleaved round-robin so box drift hits every mode alike.
+"""Same-process A/B of the drop-in upload, interleaved
+round-robin so box drift hits every mode alike: one 2^19 proof with the trace
+resident in HBM; the same proof from pageable host memory (lsp_prove, mem =
+HOST); the upload alone; the upload then the resident proof of the uploaded
+copy; and the GPU left idle for the upload's 2.4 ms, then the resident proof
+(what an idle gap alone costs the next proof: the clock's ramp).
+(profiles/r05c_time_upload.txt is the earlier form of this tool, which also
+timed registering the caller's buffer in place: no faster than pageable.)
 Usage: time_upload.py [LOG_N] [ROUNDS]"""
 import os
 import statistics
@@ -34,30 +35,35 @@ def resident():
     return ctx.prove(dp, air, pub, h, w)
 
 
-def host(pin, t=None):
-    os.environ["LSP_H2D_PIN"] = "1" if pin else "0"
-    return ctx.prove(tr if t is None else t, air, pub)
+def host(_pin=False):
+    return ctx.prove(tr, air, pub)
 
 
-fresh = [None]
+dp2 = ctx.dev_alloc(tr.nbytes)
 
 
-def host_fresh():
-    return host(True, fresh[0])
+def h2d_only():  # the upload alone (lsp_memcpy_h2d: one pageable hipMemcpyAsync + a stream sync)
+    ctx.h2d(dp2, tr)
 
 
-modes = {"resident": resident, "host_pinned": lambda: host(True), "host_pinned_fresh": host_fresh,
-         "host_pageable": lambda: host(False)}
+def h2d_then_resident():  # the same upload, then the resident proof of the uploaded copy
+    ctx.h2d(dp2, tr)
+    return ctx.prove(dp2, air, pub, h, w)
+
+
+def idle_then_resident():  # the GPU idle for as long as the upload takes, then the resident proof
+    time.sleep(0.0024)
+    return ctx.prove(dp, air, pub, h, w)
+
+
+modes = {"resident": resident, "host": lambda: host(False), "h2d_only": h2d_only,
+         "h2d_then_resident": h2d_then_resident, "idle_then_resident": idle_then_resident}
 ref = resident()
-fresh[0] = tr.copy()
-for f in modes.values():  # warm every path
-    assert f() == ref
+for k, f in modes.items():  # warm every path
+    assert k == "h2d_only" or f() == ref
 ts = {k: [] for k in modes}
 for r in range(rounds):
     for k, f in modes.items():
-        if k == "host_pinned_fresh":
-            fresh[0] = None
-            fresh[0] = tr.copy()  # new pages, written (outside the timed region)
         ctx.synchronize()
         t = time.perf_counter()
         f()
@@ -65,7 +71,9 @@ for r in range(rounds):
 med = {k: statistics.median(v) * 1e3 for k, v in ts.items()}
 print(f"log_n={log_n} trace {tr.nbytes / 2**20:.0f} MiB, {rounds} interleaved rounds, median ms: "
       + ", ".join(f"{k} {v:.2f}" for k, v in med.items()))
-for k in ("host_pinned", "host_pinned_fresh", "host_pageable"):
+for k in ("host", "h2d_then_resident", "idle_then_resident"):
     add = med[k] - med["resident"]
     print(f"{k} - resident = {add:.2f} ms ({tr.nbytes / max(add, 1e-3) / 1e6:.1f} GB/s of the proof's added time)")
+print(f"h2d_only: {med['h2d_only']:.2f} ms = {tr.nbytes / med['h2d_only'] / 1e6:.1f} GB/s")
 ctx.dev_free(dp)
+ctx.dev_free(dp2)

@@ -57,13 +57,13 @@ for step in "$@"; do
       cut -c1-600 gpurun_out/bench_$TAG.json ;;
     benchq)
       timeout -k 10 400 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --inflight 0 --shard-leg none \
-        --batch-leg none --shape-leg none --no-host-trace-leg > gpurun_out/benchq_$TAG.json \
+        --batch-leg none --shape-leg none --wide-leg 0 --no-host-trace-leg > gpurun_out/benchq_$TAG.json \
         2> gpurun_out/benchq_$TAG.err || fail "$step" gpurun_out/benchq_$TAG.err
       python -c "import json; d=json.load(open('gpurun_out/benchq_$TAG.json')); print(d['ms_per_step'], d['prove_time_median_s'], d['roofline']['ms'], d['roofline_valu']['ms'])" ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o bench -- \
         python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --inflight 0 --shard-leg none --batch-leg none \
-        --shape-leg none --no-host-trace-leg > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.err \
+        --shape-leg none --wide-leg 0 --no-host-trace-leg > gpurun_out/prof_$TAG.json 2> gpurun_out/prof_$TAG.err \
         || fail "$step" gpurun_out/prof_$TAG.err
       echo "kernel trace in gpurun_out/prof_$TAG" ;;
     pmc)

@@ -364,8 +364,25 @@ void calibrate_exchange(lsp_ctx* ctx, Comm& comm) {
         std::sort(t.begin(), t.end());
         return t[t.size() / 2];
     };
+    // the minimum of each value over the ranks: every rank then takes the same
+    // branch below and plans the same exchange (a rank-dependent branch would
+    // issue a collective some ranks skip -- RCCL hangs on that)
+    auto agree_min = [&](std::vector<double> mine) {
+        const size_t k = mine.size();
+        double* ds = (double*)ctx->buf("calib_ds", k * sizeof(double));
+        double* dr = (double*)ctx->buf("calib_dr", k * sizeof(double) * G);
+        LSP_HIP(hipMemcpyAsync(ds, mine.data(), k * sizeof(double), hipMemcpyHostToDevice, st));
+        comm.allgather(ctx, ds, dr, k * sizeof(double), "calibration");
+        std::vector<double> all(k * G);
+        LSP_HIP(hipMemcpyAsync(all.data(), dr, all.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+        LSP_HIP(hipStreamSynchronize(st));
+        for (size_t r = 1; r < G; ++r)
+            for (size_t i = 0; i < k; ++i) mine[i] = std::min(mine[i], all[r * k + i]);
+        for (size_t i = 0; i < k; ++i) mine[i] = std::min(mine[i], all[i]);
+        return mine;
+    };
     // the allgather: a 4 MiB probe first; only a transport that is not clearly
-    // below the break-even region (>= 20 GB/s) gets the 256 MiB one
+    // below the break-even region (>= 20 GB/s on every rank) gets the 256 MiB one
     auto probe = [&](size_t total) {
         const size_t share = std::max<size_t>(total / G / 256, 1) * 256;
         char* s = (char*)ctx->buf("calib_s", share);
@@ -375,7 +392,7 @@ void calibrate_exchange(lsp_ctx* ctx, Comm& comm) {
         comm.ag_probe_bytes = share * G;
         return (double)((G - 1) * share) / (ms * 1e-3) / 1e9;
     };
-    double gbs = probe((size_t)4 << 20);
+    double gbs = agree_min({probe((size_t)4 << 20)})[0];
     if (gbs >= 20) gbs = probe((size_t)256 << 20);
     // the inverse NTT the split distributes: 8 columns of 2^20 (3 passes like the proofs' sizes)
     const uint32_t logh = 20;
@@ -386,22 +403,9 @@ void calibrate_exchange(lsp_ctx* ctx, Comm& comm) {
     const uint4* tw = ctx->twiddle29(logh, true);
     const double ms =
         timed([&] { LSP_HIP(launch_intt(x, ColMap::plain((uint32_t)w), y, w, logh, tw, st)); }, 3);
-    const double rate = (double)(h * w) / (ms * 1e-3) / 1e9;
-    // agree on the minimum over the ranks (every rank then plans the same exchange)
-    double mine[2] = {gbs, rate};
-    double* ds = (double*)ctx->buf("calib_ds", sizeof mine);
-    double* dr = (double*)ctx->buf("calib_dr", sizeof mine * G);
-    LSP_HIP(hipMemcpyAsync(ds, mine, sizeof mine, hipMemcpyHostToDevice, st));
-    comm.allgather(ctx, ds, dr, sizeof mine, "calibration");
-    std::vector<double> all(2 * G);
-    LSP_HIP(hipMemcpyAsync(all.data(), dr, all.size() * sizeof(double), hipMemcpyDeviceToHost, st));
-    LSP_HIP(hipStreamSynchronize(st));
-    comm.ag_gbs = all[0];
-    comm.intt_gelem_s = all[1];
-    for (size_t r = 1; r < G; ++r) {
-        comm.ag_gbs = std::min(comm.ag_gbs, all[2 * r]);
-        comm.intt_gelem_s = std::min(comm.intt_gelem_s, all[2 * r + 1]);
-    }
+    const std::vector<double> agreed = agree_min({gbs, (double)(h * w) / (ms * 1e-3) / 1e9});
+    comm.ag_gbs = agreed[0];
+    comm.intt_gelem_s = agreed[1];
     ctx->release("calib_");
 }
 

@@ -5,7 +5,7 @@ import csv
 import sys
 
 path = sys.argv[1]
-mark = sys.argv[2] if len(sys.argv) > 2 else "k_quotient"
+mark = sys.argv[2] if len(sys.argv) > 2 else "k_open_denoms"  # once per proof
 def short(n):
     return n.replace("void ", "").replace("lsp::(anonymous namespace)::", "").replace("lsp::", "").split("(")[0][:40]
 

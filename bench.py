@@ -413,7 +413,7 @@ def main_leg(args, dist, ranks_seen):
         if table is not None:
             out.update(table)
         if shard and world > 1:
-            out["exchange"] = ctx.exchange_plan(h, w)
+            out["exchange"] = ctx.exchange_plan(h, w, q)
         if world == 1 and not shard and args.inflight > 1:
             out["inflight"] = inflight(args, cfg, air, pub, trace, ctx, dtrace)
         if world == 1 and not shard and not args.no_host_trace_leg:
@@ -725,7 +725,7 @@ def shard_leg(args, dist, ctx, sizes):
         if table is not None:
             run.update(table)
         if world > 1:  # the inverse-NTT exchange this proof chose, on the attach-time calibration
-            run["exchange"] = ctx.exchange_plan(h, w)
+            run["exchange"] = ctx.exchange_plan(h, w, 1 << air_log_q(air, cfg))
         if rank == 0:
             t = time.perf_counter()
             run["verified"] = bool(ctx.verify(proof, air, pub))

@@ -341,13 +341,14 @@ int lsp_ctx_mem_stats(lsp_ctx *ctx, size_t *pool_bytes, size_t *device_used, siz
  * 1: split by columns + an allgather of the coefficients, or a redundant
  * inverse on every rank; lsp_comm_exchange_plan) */
 int lsp_comm_selftest(lsp_ctx *ctx);
-/* the exchange plan a sharded proof of an h x w trace makes on ctx's
+/* the exchange plan a sharded proof of an h x w trace with q quotient chunks
+ * (lsp_log_quotient_degree; 0 = count the trace only) makes on ctx's
  * communicator: the calibrated allgather_gbs / intt_gelem_s (0 when the
  * communicator was never self-tested), the probe's size, split (1 = columns
  * split + allgather, 0 = redundant inverse on every rank) and the model's two
  * costs in ms.  Any output but split may be NULL.  LSP_SHARD_SPLIT_INTT=0/1
  * in the environment forces the choice. */
-int lsp_comm_exchange_plan(lsp_ctx *ctx, size_t h, size_t w, double *allgather_gbs, double *intt_gelem_s,
+int lsp_comm_exchange_plan(lsp_ctx *ctx, size_t h, size_t w, size_t q, double *allgather_gbs, double *intt_gelem_s,
                            size_t *probe_bytes, int *split, double *allgather_ms, double *redundant_ms);
 /* threads of ctx's host pool (tree tops, FRI tail, query assembly): up to 16,
  * from this process's CPU affinity set -- divided among LOCAL_WORLD_SIZE

@@ -129,7 +129,7 @@ _SIGS = {
     "lsp_ctx_set_phase_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                                 ctypes.c_size_t]),
     "lsp_comm_selftest": (ctypes.c_int, [ctypes.c_void_p]),
-    "lsp_comm_exchange_plan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+    "lsp_comm_exchange_plan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int),
                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]),

@@ -993,14 +993,15 @@ int lsp_comm_selftest(lsp_ctx* ctx) {
     });
 }
 
-int lsp_comm_exchange_plan(lsp_ctx* ctx, size_t h, size_t w, double* allgather_gbs, double* intt_gelem_s,
+int lsp_comm_exchange_plan(lsp_ctx* ctx, size_t h, size_t w, size_t q, double* allgather_gbs, double* intt_gelem_s,
                            size_t* probe_bytes, int* split, double* allgather_ms, double* redundant_ms) {
     return guarded(ctx, [&] {
         LSP_REQUIRE(ctx && split, LSP_E_ARG, "null argument");
         std::lock_guard<std::mutex> g(ctx->mu);
         LSP_REQUIRE(ctx->comm, LSP_E_STATE, "no communicator attached");
         const Comm& c = *ctx->comm;
-        const ExchangePlan p = exchange_plan(c, h, w);
+        LSP_REQUIRE(q == 0 || (q & (q - 1)) == 0, LSP_E_ARG, "q must be 0 or a power of two");
+        const ExchangePlan p = exchange_plan(c, h, w, q, ctx->log_blowup);
         if (allgather_gbs) *allgather_gbs = c.ag_gbs;
         if (intt_gelem_s) *intt_gelem_s = c.intt_gelem_s;
         if (probe_bytes) *probe_bytes = c.ag_probe_bytes;

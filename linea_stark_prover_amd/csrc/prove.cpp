@@ -320,14 +320,18 @@ static void subcoset_lde(lsp_ctx* ctx, const Fr* coef, ColMap map, size_t h, siz
 }
 
 // A sharded proof either splits the inverse NTTs by columns (rank g inverts
-// the columns bitrev(g) + G k and the coefficients are allgathered) or has
-// every rank invert every column.  The split moves (G - 1) h ceil(w/G) elements
-// into every rank and saves (w - ceil(w/G)) h elements of inverse NTT; with
-// the communicator calibrated (lsp_comm_selftest) the cheaper one is taken --
-// on the same measured numbers on every rank, so the collective schedule
-// stays rank-identical.  Uncalibrated (in-process groups, a transport never
+// the columns bitrev(g) + G k and the coefficients are allgathered; each
+// quotient holder inverts its own chunks before their broadcast) or has every
+// rank invert every trace column and, after the broadcast of the values, every
+// quotient chunk.  The split moves (G - 1) h ceil(w/G) elements into every
+// rank and saves (w - ceil(w/G)) h + (q - q/Gq) h elements of inverse NTT (the
+// quotient broadcasts carry the same bytes either way); with the communicator
+// calibrated (lsp_comm_selftest) the cheaper one is taken -- on the same
+// measured numbers on every rank, so the collective schedule stays
+// rank-identical.  Uncalibrated (in-process groups, a transport never
 // self-tested): the split.  LSP_SHARD_SPLIT_INTT=0/1 forces either (A/B).
-ExchangePlan exchange_plan(const Comm& comm, size_t h, size_t w) {
+// q = 0: the trace's share only.
+ExchangePlan exchange_plan(const Comm& comm, size_t h, size_t w, size_t q, uint32_t log_blowup) {
     // read per proof (not cached): tests flip it between proofs in one process
     const char* fe = std::getenv("LSP_SHARD_SPLIT_INTT");
     const int forced = fe && *fe ? (*fe == '0' ? 0 : 1) : -1;
@@ -335,7 +339,12 @@ ExchangePlan exchange_plan(const Comm& comm, size_t h, size_t w) {
     const size_t G = (size_t)comm.size, cg = (w + G - 1) / G;
     if (comm.ag_gbs > 0 && comm.intt_gelem_s > 0) {
         p.allgather_ms = (double)((G - 1) * h * cg * sizeof(Fr)) / (comm.ag_gbs * 1e9) * 1e3;
-        p.redundant_ms = (double)((w - std::min(w, cg)) * h) / (comm.intt_gelem_s * 1e9) * 1e3;
+        size_t qx = 0;  // quotient chunks a rank inverts beyond its own without the split
+        if (q > 0) {
+            const size_t N = h << log_blowup, S = N / G, Q = q * h, Sq = std::min(S, Q), Gq = Q / Sq;
+            qx = q - std::max<size_t>(q / Gq, 1);
+        }
+        p.redundant_ms = (double)((w - std::min(w, cg) + qx) * h) / (comm.intt_gelem_s * 1e9) * 1e3;
         p.split = p.allgather_ms < p.redundant_ms;
         p.reason = p.split ? "measured: allgather cheaper than the redundant inverse"
                            : "measured: redundant inverse cheaper than the allgather";
@@ -903,7 +912,7 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
         std::vector<Fr> shifts(std::max(w, q), GEN);
         T.begin("coset_lde_batch");
         span("coset_lde_batch", w, h, (int)lb);
-        const bool split = G > 1 && exchange_plan(comm, h, w).split;
+        const bool split = G > 1 && exchange_plan(comm, h, w, q, lb).split;
         const Fr* tcoef = nullptr;  // h * coefficients of the trace (split or sub), read through tmap
         ColMap tmap;
         if (split) {

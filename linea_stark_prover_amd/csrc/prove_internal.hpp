@@ -35,15 +35,16 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
 // GPU's inverse NTT, agree on the minimum over the ranks (comm.ag_gbs,
 // comm.intt_gelem_s)
 void calibrate_exchange(lsp_ctx* ctx, Comm& comm);
-// the inverse-NTT exchange a sharded proof of h x w over comm makes: true =
-// split by columns + an allgather of the coefficients, false = every rank
-// inverts every column (LSP_SHARD_SPLIT_INTT=0/1 forces it); rank-identical
+// the inverse-NTT exchange a sharded proof of h x w (q quotient chunks) over
+// comm makes: true = split by columns + an allgather of the coefficients,
+// false = every rank inverts every column (LSP_SHARD_SPLIT_INTT=0/1 forces
+// it); rank-identical
 struct ExchangePlan {
     bool split;
     double allgather_ms, redundant_ms;  // the model's two costs (0 when uncalibrated)
     const char* reason;
 };
-ExchangePlan exchange_plan(const Comm& comm, size_t h, size_t w);
+ExchangePlan exchange_plan(const Comm& comm, size_t h, size_t w, size_t q, uint32_t log_blowup);
 // proof wire format and field view (proof.cpp)
 // pool (optional): the queries are written in parallel (the element
 // conversions to canonical words are ~2/3 of a 2^19 proof's 10 K elements)

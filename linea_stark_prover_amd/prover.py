@@ -333,13 +333,14 @@ class Context:
             raise
         return p
 
-    def exchange_plan(self, h: int, w: int) -> dict:
+    def exchange_plan(self, h: int, w: int, q: int = 0) -> dict:
         """lsp_comm_exchange_plan: the calibrated allgather bandwidth and inverse-NTT
         rate of the attached communicator and the inverse-NTT exchange a sharded
-        proof of h x w takes on them"""
+        proof of h x w with q quotient chunks takes on them (q = 0: the trace's
+        share of the model only)"""
         gbs, rate, ms_ag, ms_red = ctypes.c_double(), ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
         probe, split = ctypes.c_size_t(), ctypes.c_int()
-        self._chk(L.lib().lsp_comm_exchange_plan(self.h, h, w, ctypes.byref(gbs), ctypes.byref(rate),
+        self._chk(L.lib().lsp_comm_exchange_plan(self.h, h, w, q, ctypes.byref(gbs), ctypes.byref(rate),
                                                  ctypes.byref(probe), ctypes.byref(split), ctypes.byref(ms_ag),
                                                  ctypes.byref(ms_red)))
         return {"allgather_gbs": gbs.value, "intt_gelem_per_s": rate.value, "probe_bytes": probe.value,

@@ -340,7 +340,7 @@ ExchangePlan exchange_plan(const Comm& comm, size_t h, size_t w, size_t q, uint3
     if (comm.ag_gbs > 0 && comm.intt_gelem_s > 0) {
         p.allgather_ms = (double)((G - 1) * h * cg * sizeof(Fr)) / (comm.ag_gbs * 1e9) * 1e3;
         size_t qx = 0;  // quotient chunks a rank inverts beyond its own without the split
-        if (q > 0) {
+        if (q > 0 && G <= ((size_t)1 << log_blowup)) {  // (more ranks than cosets: every rank inverts them anyway)
             const size_t N = h << log_blowup, S = N / G, Q = q * h, Sq = std::min(S, Q), Gq = Q / Sq;
             qx = q - std::max<size_t>(q / Gq, 1);
         }

@@ -13,6 +13,55 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: larger sizes")
 
 
+# Long oracle proofs started in the background as soon as their tests are
+# selected (tests/oracle_job.py), so they overlap the rest of the suite:
+# test id suffix -> (log_n, threads).  LSP_ORACLE_PRESTART=0 computes them
+# inline instead.
+ORACLE_JOBS = {"test_configs1_whole_proof_2e22_vs_oracle": (22, 16)}
+_jobs = {}  # test name -> (Popen, output path)
+
+
+@pytest.hookimpl(trylast=True)  # after -m / -k deselection: only tests that will run
+def pytest_collection_modifyitems(session, config, items):
+    if os.environ.get("LSP_ORACLE_PRESTART", "1") == "0" or config.getoption("collectonly"):
+        return
+    import subprocess
+    import tempfile
+    names = {item.name for item in items}
+    for name, (log_n, threads) in ORACLE_JOBS.items():
+        if name not in names or name in _jobs:
+            continue
+        out = os.path.join(tempfile.mkdtemp(prefix="lsp_oracle_"), f"proof_{log_n}.bin")
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+        proc = subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "oracle_job.py"), str(log_n),
+                                 str(threads), out], env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+        _jobs[name] = (proc, out)
+
+
+def pytest_sessionfinish(session, exitstatus):
+    for proc, _ in _jobs.values():
+        if proc.poll() is None:
+            proc.kill()
+            proc.wait()
+
+
+def oracle_job_result(name, timeout=1800):
+    """The background job's proof bytes (waits for it), or None when no job was
+    started (LSP_ORACLE_PRESTART=0, or the test was run some other way)."""
+    if name not in _jobs:
+        return None
+    proc, out = _jobs[name]
+    try:
+        _, err = proc.communicate(timeout=timeout)
+    except Exception:
+        proc.kill()
+        raise
+    if proc.returncode != 0 or not os.path.exists(out):
+        raise RuntimeError(f"oracle job for {name} failed (rc {proc.returncode}): {err.decode()[-2000:]}")
+    with open(out, "rb") as f:
+        return f.read()
+
+
 @pytest.fixture(scope="session")
 def oracle_lib():
     from oracle import cref

@@ -14,50 +14,59 @@ def pytest_configure(config):
 
 
 # Long oracle proofs started in the background as soon as their tests are
-# selected (tests/oracle_job.py), so they overlap the rest of the suite:
-# test id suffix -> (log_n, threads).  LSP_ORACLE_PRESTART=0 computes them
-# inline instead.
-ORACLE_JOBS = {"test_configs1_whole_proof_2e22_vs_oracle": (22, 16)}
-_jobs = {}  # test name -> (Popen, output path)
+# selected (tests/oracle_job.py: one process, the jobs in this order), so they
+# overlap the rest of the suite: test name -> (log_n, ncols).
+# LSP_ORACLE_PRESTART=0 computes them inline instead.
+ORACLE_JOBS = {"test_benchlog_shape_whole_proof_2e19_vs_oracle": (19, 6),
+               "test_configs1_whole_proof_2e22_vs_oracle": (22, 3)}
+ORACLE_THREADS = min(16, os.cpu_count() or 1)  # the GPU box's CPU share (os.cpu_count() shows the whole machine)
+_job = {}  # "proc", "err" (stderr file), "out": test name -> proof path
 
 
 @pytest.hookimpl(trylast=True)  # after -m / -k deselection: only tests that will run
 def pytest_collection_modifyitems(session, config, items):
-    if os.environ.get("LSP_ORACLE_PRESTART", "1") == "0" or config.getoption("collectonly"):
+    if os.environ.get("LSP_ORACLE_PRESTART", "1") == "0" or config.getoption("collectonly") or _job:
         return
     import subprocess
     import tempfile
     names = {item.name for item in items}
-    for name, (log_n, threads) in ORACLE_JOBS.items():
-        if name not in names or name in _jobs:
-            continue
-        out = os.path.join(tempfile.mkdtemp(prefix="lsp_oracle_"), f"proof_{log_n}.bin")
-        env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-        proc = subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "oracle_job.py"), str(log_n),
-                                 str(threads), out], env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
-        _jobs[name] = (proc, out)
+    sel = [(n, j) for n, j in ORACLE_JOBS.items() if n in names]
+    if not sel:
+        return
+    tmp = tempfile.mkdtemp(prefix="lsp_oracle_")
+    out = {n: os.path.join(tmp, f"{n}.bin") for n, _ in sel}
+    err = open(os.path.join(tmp, "stderr.txt"), "w+b")
+    env = dict(os.environ, OMP_NUM_THREADS=str(ORACLE_THREADS))
+    cmd = [sys.executable, os.path.join(ROOT, "tests", "oracle_job.py"), str(ORACLE_THREADS)]
+    cmd += [f"{out[n]}:{log_n}:{ncols}" for n, (log_n, ncols) in sel]
+    _job.update(proc=subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=err), err=err, out=out)
 
 
 def pytest_sessionfinish(session, exitstatus):
-    for proc, _ in _jobs.values():
-        if proc.poll() is None:
-            proc.kill()
-            proc.wait()
+    proc = _job.get("proc")
+    if proc is not None and proc.poll() is None:
+        proc.kill()
+        proc.wait()
 
 
 def oracle_job_result(name, timeout=1800):
-    """The background job's proof bytes (waits for it), or None when no job was
-    started (LSP_ORACLE_PRESTART=0, or the test was run some other way)."""
-    if name not in _jobs:
+    """The background job's proof bytes for test `name` (waits for them), or
+    None when no job was started for it (LSP_ORACLE_PRESTART=0, or the test
+    was run some other way)."""
+    import time
+    if name not in _job.get("out", {}):
         return None
-    proc, out = _jobs[name]
-    try:
-        _, err = proc.communicate(timeout=timeout)
-    except Exception:
-        proc.kill()
-        raise
-    if proc.returncode != 0 or not os.path.exists(out):
-        raise RuntimeError(f"oracle job for {name} failed (rc {proc.returncode}): {err.decode()[-2000:]}")
+    proc, out = _job["proc"], _job["out"][name]
+    t0 = time.time()
+    while not os.path.exists(out):
+        if proc.poll() is not None and not os.path.exists(out):
+            _job["err"].seek(0)
+            tail = _job["err"].read().decode(errors="replace")[-2000:]
+            raise RuntimeError(f"oracle job for {name} ended without it (rc {proc.returncode}): {tail}")
+        if time.time() - t0 > timeout:
+            proc.kill()
+            raise TimeoutError(f"oracle job for {name}: no proof after {timeout} s")
+        time.sleep(0.2)
     with open(out, "rb") as f:
         return f.read()
 

@@ -1,8 +1,10 @@
-"""Background oracle job for tests/test_gpu_fullsize_oracle.py: the C oracle's
-whole proof of the seeded 3x3 permutation trace at 2^LOG_N rows, written to
-OUT.  conftest.py starts it when the test is selected, so its ~5 minutes of
-host work overlap the rest of the GPU suite instead of adding to it.
-Usage: python tests/oracle_job.py LOG_N THREADS OUT"""
+"""Background oracle jobs for tests/test_gpu_fullsize_oracle.py: the C oracle's
+whole proofs of seeded NCOLS x NCOLS permutation traces, one after another,
+each written to its OUT file (atomically: the reader sees a whole proof or
+nothing).  conftest.py starts this when the tests are selected, so the
+oracle's minutes of host work overlap the rest of the GPU suite instead of
+adding to it.
+Usage: python tests/oracle_job.py THREADS OUT:LOG_N:NCOLS [OUT:LOG_N:NCOLS ...]"""
 import os
 import sys
 
@@ -12,14 +14,18 @@ from oracle import cref  # noqa: E402
 
 
 def main():
-    log_n, threads, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+    threads = int(sys.argv[1])
     p = cref.setup()
-    tb, w = cref.gen_perm_trace(p, log_n, 3)
-    proof = cref.prove(p, tb, 1 << log_n, w, cref.perm_air(3), nthreads=threads)
-    tmp = out + ".part"
-    with open(tmp, "wb") as f:
-        f.write(proof)
-    os.replace(tmp, out)  # the reader sees the whole proof or nothing
+    for job in sys.argv[2:]:
+        out, log_n, ncols = job.rsplit(":", 2)
+        log_n, ncols = int(log_n), int(ncols)
+        tb, w = cref.gen_perm_trace(p, log_n, ncols)
+        proof = cref.prove(p, tb, 1 << log_n, w, cref.perm_air(ncols), nthreads=threads)
+        del tb
+        tmp = out + ".part"
+        with open(tmp, "wb") as f:
+            f.write(proof)
+        os.replace(tmp, out)
 
 
 if __name__ == "__main__":

@@ -1,5 +1,6 @@
 """Whole-proof parity of BASELINE configs[1] and configs[2] at their full sizes,
-on the library under test (VERDICT r4 "next" #1).
+and of bench.log's 6+6 shape at 2^19, on the library under test (VERDICT r4
+"next" #1).
 
 * configs[1]: the 3x3 permutation AIR at 2^22 rows.  The GPU proof of the
   seeded trace (uploaded from host memory, as the reference's `prove` takes
@@ -41,25 +42,35 @@ def _p(a):
     return ctypes.c_void_p(a.ctypes.data)
 
 
-@pytest.mark.timeout(900)  # ~5 minutes of oracle proof; runners pass --timeout 120..300 per test
-def test_configs1_whole_proof_2e22_vs_oracle(gpu_ctx, oracle_lib, heartbeat):
+def _whole_proof_vs_oracle(gpu_ctx, oracle_lib, heartbeat, name, log_n, ncols):
     from linea_stark_prover_amd.air import permutation_air
-    log_n = 22
     p = oracle_lib.setup()
-    tb, w = oracle_lib.gen_perm_trace(p, log_n, 3)
+    tb, w = oracle_lib.gen_perm_trace(p, log_n, ncols)
     trace = np.frombuffer(tb, dtype=np.uint64).reshape(1 << log_n, w, 4)
     pub = np.concatenate([np.array(p.alpha, np.uint64).reshape(1, 4), np.array(p.delta, np.uint64).reshape(1, 4)])
-    proof = gpu_ctx.prove(trace, permutation_air(3), pub)
-    assert gpu_ctx.verify(proof, permutation_air(3), pub)
+    proof = gpu_ctx.prove(trace, permutation_air(ncols), pub)
+    assert gpu_ctx.verify(proof, permutation_air(ncols), pub)
     from conftest import oracle_job_result
-    with heartbeat("C oracle proving 2^22 rows"):
+    with heartbeat(f"C oracle proving 2^{log_n} rows of the {ncols}x{ncols} AIR"):
         # started in the background at collection (tests/oracle_job.py: the same
         # seeded trace and oracle call), else computed here
-        expect = oracle_job_result("test_configs1_whole_proof_2e22_vs_oracle")
+        expect = oracle_job_result(name)
         if expect is None:
-            expect = oracle_lib.prove(p, tb, 1 << log_n, w, oracle_lib.perm_air(3), nthreads=THREADS)
+            expect = oracle_lib.prove(p, tb, 1 << log_n, w, oracle_lib.perm_air(ncols), nthreads=THREADS)
     assert len(proof) == len(expect)
     assert proof == expect
+
+
+@pytest.mark.timeout(600)
+def test_benchlog_shape_whole_proof_2e19_vs_oracle(gpu_ctx, oracle_lib, heartbeat):
+    """bench.log's measured shape (6+6 columns, w = 14, q = 8 chunks: bench.log:1-30), the
+    bench's shape_bench_log leg, at its full 2^19 rows (about a minute of oracle)"""
+    _whole_proof_vs_oracle(gpu_ctx, oracle_lib, heartbeat, "test_benchlog_shape_whole_proof_2e19_vs_oracle", 19, 6)
+
+
+@pytest.mark.timeout(900)  # ~5 minutes of oracle proof; runners pass --timeout 120..300 per test
+def test_configs1_whole_proof_2e22_vs_oracle(gpu_ctx, oracle_lib, heartbeat):
+    _whole_proof_vs_oracle(gpu_ctx, oracle_lib, heartbeat, "test_configs1_whole_proof_2e22_vs_oracle", 22, 3)
 
 
 def _replay(proof_bytes, pub_ints, perm):

@@ -235,3 +235,21 @@ def test_eval_points_matches_lde(oracle_lib, logh, w, added):
     got = np.zeros((N, w, 4), np.uint64)
     L.lo_eval_points(P(mat), ctypes.c_size_t(h), ctypes.c_size_t(w), P(xs), ctypes.c_size_t(N), P(got), 4)
     assert np.array_equal(got, lde)
+
+
+def test_background_oracle_job_matches_direct_call(oracle_lib, tmp_path):
+    """tests/oracle_job.py (the GPU suite's background oracle proofs): jobs run
+    in order, each proof written whole, equal to calling the oracle directly"""
+    import subprocess
+    import sys
+    jobs = [(str(tmp_path / "a.bin"), 6, 3), (str(tmp_path / "b.bin"), 5, 6)]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run([sys.executable, os.path.join(root, "tests", "oracle_job.py"), "2"] +
+                   [f"{o}:{n}:{c}" for o, n, c in jobs], check=True, timeout=300)
+    p = oracle_lib.setup()
+    for out, log_n, ncols in jobs:
+        tb, w = oracle_lib.gen_perm_trace(p, log_n, ncols)
+        expect = oracle_lib.prove(p, tb, 1 << log_n, w, oracle_lib.perm_air(ncols), nthreads=2)
+        with open(out, "rb") as f:
+            assert f.read() == expect
+        assert not os.path.exists(out + ".part")

@@ -107,10 +107,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-log-n", type=int, default=None,
                     help="CPU-baseline size (rows = 2^cpu_log_n; default: the headline's --log-n, BASELINE.md's "
                          "2^19 input)")
-    ap.add_argument("--cpu-runs", type=int, default=3, help="CPU-baseline timed runs (median)")
-    ap.add_argument("--cpu-warmup", type=int, default=0,
-                    help="untimed CPU-baseline runs first (0: the C restatement has no JIT or cache to warm; each "
-                         "run allocates and faults in its own buffers)")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="CPU-baseline timed runs (median; BASELINE.md's plan: 5)")
+    ap.add_argument("--cpu-warmup", type=int, default=1,
+                    help="untimed CPU-baseline runs first (BASELINE.md's plan: 1; about 10 s each at 2^19)")
     ap.add_argument("--cpu-small-log-n", type=int, default=0,
                     help="an extra, smaller CPU sample reported beside the headline one (0, the default, disables: "
                          "the headline-size sample is the baseline)")

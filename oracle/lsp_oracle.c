@@ -221,6 +221,25 @@ static uint32_t log2_strict(size_t n) {
     return ((size_t)1 << b) == n ? b : 0xFFFFFFFFu;
 }
 
+/* ------------------------------------------------------------ phase timer */
+/* LO_TIME=1: lo_prove prints each phase's wall time to stderr (profiling the
+ * checker itself; off by default) */
+#include <stdio.h>
+#include <time.h>
+static double lo_now(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+static void lo_phase(const char *name, double *t0) {
+    static int on = -1;
+    if (on < 0) on = getenv("LO_TIME") != NULL;
+    if (!on) return;
+    double t = lo_now();
+    fprintf(stderr, "[oracle] %-28s %8.3f s\n", name, t - *t0);
+    *t0 = t;
+}
+
 /* ---------------------------------------------------------------- threads */
 typedef void (*range_fn)(void *ctx, size_t lo, size_t hi);
 typedef struct { range_fn fn; void *ctx; size_t lo, hi; } job_t;
@@ -320,9 +339,17 @@ void lo_setup(uint64_t seed, uint32_t sbox_degree, uint32_t rounds_f, uint32_t r
 }
 
 /* -------------------------------------------------------------- Poseidon2 */
+/* x^D (D = sbox_degree: 11, or 17 for the other BLS12-377 instance) by
+ * left-to-right square-and-multiply over D's own bits: 3 squares and 2
+ * products for D = 11 (fpow64 would walk a 256-bit exponent from the top) */
 static inline void sbox(const lo_params *p, lo_fr *x) {
-    lo_fr r;
-    fpow64(x, p->sbox_degree, &r);
+    const uint32_t d = p->sbox_degree;
+    const lo_fr b = *x;
+    lo_fr r = b;
+    for (int k = 30 - __builtin_clz(d); k >= 0; --k) {
+        fmul(&r, &r, &r);
+        if ((d >> k) & 1) fmul(&r, &b, &r);
+    }
     *x = r;
 }
 /* generic U2/U3 layers (lo_params.generic_lin) */
@@ -443,36 +470,79 @@ void lo_merkle_commit(const lo_params *p, const lo_fr *rows, size_t h, size_t W,
 }
 
 /* ------------------------------------------------------------------- NTT */
-/* natural-order in-place DFT with root w (order n) */
-static void ntt_inplace(lo_fr *a, size_t n, const lo_fr *root) {
-    uint32_t lg = log2_strict(n);
-    for (size_t i = 0; i < n; ++i) {
-        size_t j = (size_t)bitrev64(i, lg);
-        if (j > i) {
-            lo_fr t = a[i];
-            a[i] = a[j];
-            a[j] = t;
-        }
-    }
-    for (size_t len = 2; len <= n; len <<= 1) {
-        lo_fr wl;
-        fpow64(root, n / len, &wl);
-        for (size_t i = 0; i < n; i += len) {
-            lo_fr w = ONE;
-            for (size_t j = 0; j < len / 2; ++j) {
-                lo_fr u = a[i + j], v;
-                fmul(&a[i + j + len / 2], &w, &v);
-                fadd(&u, &v, &a[i + j]);
-                fsub(&u, &v, &a[i + j + len / 2]);
-                fmul(&w, &wl, &w);
-            }
+/* natural-order in-place DFT with root w (order n): bit-reversal, then
+ * radix-2 DIT stages.  With nthreads > 1 each stage's n/2 butterflies (and the
+ * bit-reversal) are split over threads -- the same butterflies, the same
+ * twiddles, so the same result bits for any thread count. */
+typedef struct { lo_fr *a; size_t n, half; uint32_t lg; lo_fr wl; } ntt_ctx;
+static void ntt_bitrev_range(void *c, size_t lo, size_t hi) {
+    ntt_ctx *t = (ntt_ctx *)c;
+    for (size_t i = lo; i < hi; ++i) {
+        size_t j = (size_t)bitrev64(i, t->lg);
+        if (j > i) { /* the pair belongs to the range holding i */
+            lo_fr x = t->a[i];
+            t->a[i] = t->a[j];
+            t->a[j] = x;
         }
     }
 }
+static void ntt_stage_range(void *c, size_t lo, size_t hi) {
+    /* butterflies k in [lo, hi): block k / half, offset j = k % half */
+    ntt_ctx *t = (ntt_ctx *)c;
+    size_t half = t->half, j = lo % half;
+    lo_fr w;
+    fpow64(&t->wl, j, &w);
+    for (size_t k = lo; k < hi; ++k) {
+        size_t i = (k / half) * 2 * half + j;
+        lo_fr u = t->a[i], v;
+        fmul(&t->a[i + half], &w, &v);
+        fadd(&u, &v, &t->a[i]);
+        fsub(&u, &v, &t->a[i + half]);
+        if (++j == half) {
+            j = 0;
+            w = ONE;
+        } else {
+            fmul(&w, &t->wl, &w);
+        }
+    }
+}
+static void ntt_inplace_mt(lo_fr *a, size_t n, const lo_fr *root, int nthreads) {
+    ntt_ctx c = {a, n, 0, log2_strict(n), ONE};
+    parallel_for(n, nthreads, ntt_bitrev_range, &c);
+    for (size_t len = 2; len <= n; len <<= 1) {
+        fpow64(root, n / len, &c.wl);
+        c.half = len / 2;
+        parallel_for(n / 2, nthreads, ntt_stage_range, &c);
+    }
+}
+static void ntt_inplace(lo_fr *a, size_t n, const lo_fr *root) { ntt_inplace_mt(a, n, root, 1); }
 
 typedef struct {
     const lo_fr *in; size_t h, w; uint32_t added; const lo_fr *shifts; lo_fr *out;
+    int ntt_threads; /* threads inside each column's NTTs (1: columns run in parallel instead) */
 } lde_ctx;
+/* coefficient i of column col times shift^i / h, and the zero padding */
+typedef struct { lo_fr *buf; size_t h, N; lo_fr hinv, shift; } twist_ctx;
+static void twist_range(void *c, size_t lo, size_t hi) {
+    twist_ctx *t = (twist_ctx *)c;
+    lo_fr s;
+    fpow64(&t->shift, lo, &s);
+    fmul(&s, &t->hinv, &s);
+    for (size_t i = lo; i < hi; ++i) {
+        if (i < t->h) {
+            fmul(&t->buf[i], &s, &t->buf[i]);
+            fmul(&s, &t->shift, &s);
+        } else {
+            t->buf[i] = ZERO_FR;
+        }
+    }
+}
+/* output row i of column col = buf[bitrev(i)] (the bit-reversed LDE) */
+typedef struct { const lo_fr *buf; lo_fr *out; size_t w, col; uint32_t lgN; } scatter_ctx;
+static void scatter_range(void *c, size_t lo, size_t hi) {
+    scatter_ctx *t = (scatter_ctx *)c;
+    for (size_t i = lo; i < hi; ++i) t->out[i * t->w + t->col] = t->buf[bitrev64(i, t->lgN)];
+}
 static void lde_cols(void *c, size_t lo, size_t hi) {
     lde_ctx *L = (lde_ctx *)c;
     size_t h = L->h, N = h << L->added;
@@ -486,24 +556,28 @@ static void lde_cols(void *c, size_t lo, size_t hi) {
     finv(&hf, &hinv);
     for (size_t col = lo; col < hi; ++col) {
         for (size_t i = 0; i < h; ++i) buf[i] = L->in[i * L->w + col];
-        ntt_inplace(buf, h, &wh_inv); /* h * coefficients */
-        lo_fr s = hinv;               /* shift^i / h */
-        for (size_t i = 0; i < h; ++i) {
-            fmul(&buf[i], &s, &buf[i]);
-            fmul(&s, &L->shifts[col], &s);
-        }
-        for (size_t i = h; i < N; ++i) buf[i] = ZERO_FR;
-        ntt_inplace(buf, N, &wN);
-        for (size_t i = 0; i < N; ++i) L->out[i * L->w + col] = buf[bitrev64(i, lgN)];
+        ntt_inplace_mt(buf, h, &wh_inv, L->ntt_threads); /* h * coefficients */
+        twist_ctx tc = {buf, h, N, hinv, L->shifts[col]};  /* shift^i / h, then zeros */
+        parallel_for(N, L->ntt_threads, twist_range, &tc);
+        ntt_inplace_mt(buf, N, &wN, L->ntt_threads);
+        scatter_ctx sc = {buf, L->out, L->w, col, lgN};
+        parallel_for(N, L->ntt_threads, scatter_range, &sc);
     }
     free(buf);
 }
+/* Columns in parallel when there are at least as many as threads (or the
+ * transform is small); otherwise one column at a time with each NTT stage
+ * split over the threads (the quotient's 4 chunks, the 3x3 trace's 8 columns
+ * on 16 threads). */
 void lo_coset_lde_batch(const lo_fr *in, size_t h, size_t w, uint32_t added_bits,
                         const lo_fr *shifts, lo_fr *out, int nthreads) {
     field_init();
-    lde_ctx c = {in, h, w, added_bits, shifts, out};
-    if (nthreads > (int)w) nthreads = (int)w;
-    /* parallel over columns (chunk of 1 column per thread when possible) */
+    lde_ctx c = {in, h, w, added_bits, shifts, out, 1};
+    if (nthreads > 1 && (size_t)nthreads > w && (h << added_bits) >= ((size_t)1 << 14)) {
+        c.ntt_threads = nthreads;
+        lde_cols(&c, 0, w);
+        return;
+    }
     if (nthreads <= 1 || w < 2) {
         lde_cols(&c, 0, w);
         return;
@@ -985,14 +1059,17 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
     size_t N = h << lb, Q = h << log_q;
     uint32_t logN = log_h + lb, logQ = log_h + log_q;
 
+    double tph = lo_now();
     /* ---- commit to trace data */
     lo_fr *shifts = (lo_fr *)malloc(sizeof(lo_fr) * (w > q ? w : q));
     for (size_t c = 0; c < w; ++c) shifts[c] = GEN;
     lo_fr *lde = (lo_fr *)malloc(sizeof(lo_fr) * N * w);
     lo_coset_lde_batch(trace, h, w, lb, shifts, lde, nthreads);
+    lo_phase("trace LDE", &tph);
     lo_fr *tlay = (lo_fr *)malloc(sizeof(lo_fr) * (2 * N - 1));
     lo_merkle_commit(p, lde, N, w, tlay, nthreads);
     lo_fr troot = tlay[2 * N - 2];
+    lo_phase("trace tree", &tph);
 
     chal_t *ch = (chal_t *)malloc(sizeof(chal_t));
     ch_init(ch, p, fri->transcript);
@@ -1033,10 +1110,12 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
         fmul(&first[i], &zh[i % per], &first[i]);
         fmul(&last[i], &zh[i % per], &last[i]);
     }
+    lo_phase("quotient selectors", &tph);
     lo_fr *qv = (lo_fr *)malloc(sizeof(lo_fr) * Q);
     q_ctx qc = {cfgs, ncfg, lde, w, logQ, log_q, first, last, trans, invz, &p->alpha, &p->delta, &alpha, qv, Q};
     parallel_for(Q, nthreads, q_range, &qc);
     free(xsq); free(first); free(last); free(trans); free(tmp); free(zh); free(invz);
+    lo_phase("quotient values", &tph);
 
     /* ---- commit to quotient chunks: qv viewed as h x q row-major */
     lo_fr gq = two_adic_gen(logQ), gqinv;
@@ -1045,9 +1124,11 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
     for (size_t j = 1; j < q; ++j) fmul(&shifts[j - 1], &gqinv, &shifts[j]);
     lo_fr *qlde = (lo_fr *)malloc(sizeof(lo_fr) * N * q);
     lo_coset_lde_batch(qv, h, q, lb, shifts, qlde, nthreads);
+    lo_phase("quotient LDE", &tph);
     lo_fr *qlay = (lo_fr *)malloc(sizeof(lo_fr) * (2 * N - 1));
     lo_merkle_commit(p, qlde, N, q, qlay, nthreads);
     lo_fr qroot = qlay[2 * N - 2];
+    lo_phase("quotient tree", &tph);
     ch_observe(ch, &qroot);
     lo_fr zeta = ch_sample(ch), zeta_next;
     fmul(&zeta, &wh, &zeta_next);
@@ -1066,6 +1147,7 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
     parallel_for(N, nthreads, den_range, &dc);
     batch_inverse(den, invd_zn, N, nthreads);
     free(den);
+    lo_phase("open: points, inverses", &tph);
 
     lo_fr *ys_z = (lo_fr *)malloc(sizeof(lo_fr) * w), *ys_zn = (lo_fr *)malloc(sizeof(lo_fr) * w),
           *ys_q = (lo_fr *)malloc(sizeof(lo_fr) * q);
@@ -1078,6 +1160,7 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
         for (size_t j = 0; j < q; ++j) ch_observe(ch, &ys_q[j]);
     }
     lo_fr alpha_fri = ch_sample(ch);
+    lo_phase("open: opened values", &tph);
 
     size_t nap = 2 * w + q + 1;
     lo_fr *apw = (lo_fr *)malloc(sizeof(lo_fr) * nap);
@@ -1099,6 +1182,7 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
     parallel_for(N, nthreads, red_range, &rc);
     if (dbg && dbg->fri_input) memcpy(dbg->fri_input, ro, sizeof(lo_fr) * N);
     free(invd_z); free(invd_zn); free(xs);
+    lo_phase("open: reduce rows", &tph);
 
     /* ---- FRI commit phase */
     size_t final_len = (size_t)1 << (lb + fri->log_final_poly_len);
@@ -1153,6 +1237,7 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
         if (!fis_zero(&fin[i])) return -4; /* final poly degree too high */
     if (!(fri->transcript & LO_T_SKIP_FINAL_POLY))
         for (size_t i = 0; i < flen; ++i) ch_observe(ch, &fin[i]);
+    lo_phase("FRI commit phase", &tph);
     uint64_t pw = ch_grind(ch, fri->pow_bits);
     if (cur != ro) free(cur);
 
@@ -1203,6 +1288,7 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
     for (uint32_t r = 0; r < nrounds; ++r) free(flay[r]);
     free(flay); free(froots); free(fin); free(apw); free(ro); free(ys_z); free(ys_zn); free(ys_q);
     free(qlde); free(qlay); free(qv); free(lde); free(tlay); free(shifts); free(ch);
+    lo_phase("grind, queries, serialize", &tph);
     *proof_out = b.b;
     *proof_len = b.n;
     return 0;

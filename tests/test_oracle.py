@@ -253,3 +253,33 @@ def test_background_oracle_job_matches_direct_call(oracle_lib, tmp_path):
         with open(out, "rb") as f:
             assert f.read() == expect
         assert not os.path.exists(out + ".part")
+
+
+def test_lde_thread_split_is_bit_exact(oracle_lib):
+    """lo_coset_lde_batch with each NTT stage split over threads (fewer columns
+    than threads, N >= 2^14) equals the column-parallel transform bit for bit,
+    and sampled rows equal barycentric evaluation (lo_eval_points)"""
+    import ctypes
+    import numpy as np
+    L = oracle_lib.lib()
+    P = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+    logh, w, added = 12, 3, 3
+    h, N = 1 << logh, 1 << (logh + added)
+    rng = np.random.default_rng(7)
+    mat = rng.integers(0, 2**63, size=(h, w, 4), dtype=np.uint64)
+    mat[..., 3] &= (1 << 59) - 1  # < r
+    shift = np.array([22, 0, 0, 0], np.uint64)
+    shifts = np.repeat(shift.reshape(1, 4), w, axis=0).copy()
+    outs = []
+    for th in (1, 2, 6):  # 1: one thread; 2: columns in parallel; 6 > w: stages split
+        out = np.zeros((N, w, 4), np.uint64)
+        L.lo_coset_lde_batch(P(mat), ctypes.c_size_t(h), ctypes.c_size_t(w), added, P(shifts), P(out), th)
+        outs.append(out)
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
+    rows = [0, 1, 2, N // 2 + 3, N - 1, 12345]
+    xs = np.zeros((len(rows), 4), np.uint64)
+    for k, j in enumerate(rows):
+        L.lo_lde_point(ctypes.c_size_t(h), added, P(shift), ctypes.c_uint64(j), P(xs[k]))
+    got = np.zeros((len(rows), w, 4), np.uint64)
+    L.lo_eval_points(P(mat), ctypes.c_size_t(h), ctypes.c_size_t(w), P(xs), ctypes.c_size_t(len(rows)), P(got), 4)
+    assert np.array_equal(got, outs[2][rows])

@@ -994,6 +994,13 @@ static void powers(lo_fr base, size_t n, lo_fr *dst, int nthreads) {
     parallel_for(n, nthreads, pow_range, &c);
 }
 
+/* the LDE's points in row order: xs[i] = GEN w_N^bitrev(i) */
+typedef struct { const lo_fr *nat; lo_fr *xs; uint32_t logN; } xs_ctx;
+static void xs_range(void *c, size_t lo, size_t hi) {
+    xs_ctx *x = (xs_ctx *)c;
+    for (size_t i = lo; i < hi; ++i) fmul(&GEN, &x->nat[bitrev64(i, x->logN)], &x->xs[i]);
+}
+
 typedef struct { const lo_fr *xs; lo_fr z; lo_fr *out; } den_ctx;
 static void den_range(void *c, size_t lo, size_t hi) {
     den_ctx *d = (den_ctx *)c;
@@ -1136,7 +1143,8 @@ int lo_prove(const lo_params *p, const lo_fri *fri, const lo_fr *trace, size_t h
     /* ---- open (alpha_fri is sampled after the opened values: U7) */
     lo_fr *xs = (lo_fr *)malloc(sizeof(lo_fr) * N), *xs_nat = (lo_fr *)malloc(sizeof(lo_fr) * N);
     powers(two_adic_gen(logN), N, xs_nat, nthreads);
-    for (size_t i = 0; i < N; ++i) fmul(&GEN, &xs_nat[bitrev64(i, logN)], &xs[i]);
+    xs_ctx xc = {xs_nat, xs, logN};
+    parallel_for(N, nthreads, xs_range, &xc);
     free(xs_nat);
     lo_fr *den = (lo_fr *)malloc(sizeof(lo_fr) * N), *invd_z = (lo_fr *)malloc(sizeof(lo_fr) * N),
           *invd_zn = (lo_fr *)malloc(sizeof(lo_fr) * N);

@@ -24,7 +24,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:?usage: tools/gpu.sh TAG STEP...}
 shift
-PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+PYT="python -u -m pytest -x -q --timeout 300 --timeout-method thread --durations=30"
 
 fail() { echo "FAILED: $1"; tail -40 "$2"; exit 1; }
 

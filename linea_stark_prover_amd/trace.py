@@ -54,15 +54,6 @@ def _col(c) -> np.ndarray:
     return _fr_arr(c).reshape(-1, 4)
 
 
-def _pad(c: np.ndarray, n: int) -> np.ndarray:
-    """Vec::resize(n, [0u8; 32])"""
-    if c.shape[0] == n:
-        return c
-    out = np.zeros((n, 4), np.uint64)
-    out[:c.shape[0]] = c
-    return out
-
-
 @dataclass
 class RawPermutationTrace:
     a: List[np.ndarray]
@@ -151,14 +142,23 @@ class RawTrace:
         if self.ptr is not None:
             self.ctx.dev_free(self.ptr)
         self.ptr = self.ctx.dev_alloc(h * self.width * 32)
-        cfgs, col = [], 0
-        for lt in lookup_traces:  # lookups first (trace/src/lib.rs:81-89)
-            cfg = self._push_lookup(lt, col)
-            cfgs.append(cfg)
-            col += lt.width()
-        for pt in permutation_traces:
-            cfgs.append(self._push_permutation(pt, col))
-            col += pt.width()
+        # one device buffer for the raw columns of every block in turn (the
+        # largest block's), instead of an allocation and a synchronizing free per block
+        raw = [len(t.a) + sum(len(x) for x in t.b) + 1 + len(t.b) for t in lookup_traces] + \
+              [len(t.a) + len(t.b) for t in permutation_traces]
+        self._scratch = self.ctx.dev_alloc(max(max(raw, default=1) * h * 32, 32))
+        try:
+            cfgs, col = [], 0
+            for lt in lookup_traces:  # lookups first (trace/src/lib.rs:81-89)
+                cfg = self._push_lookup(lt, col)
+                cfgs.append(cfg)
+                col += lt.width()
+            for pt in permutation_traces:
+                cfgs.append(self._push_permutation(pt, col))
+                col += pt.width()
+        finally:
+            self.ctx.dev_free(self._scratch)
+            self._scratch = None
         return cfgs
 
     def air(self, cfgs) -> LineaAIR:
@@ -166,18 +166,13 @@ class RawTrace:
 
     def _push_permutation(self, pt: RawPermutationTrace, col0: int) -> AirPermutationConfig:
         n = self.height
-        a = np.ascontiguousarray(np.stack([_pad(_col(c), n) for c in pt.a]))
-        b = np.ascontiguousarray(np.stack([_pad(_col(c), n) for c in pt.b]))
-        na, nb = a.shape[0], b.shape[0]
-        da = self._upload(a)
-        db = self._upload(b)
-        try:
-            self.ctx._chk(L.lib().lsp_witness_permutation(
-                self.ctx.h, da, na, db, nb, n, _ptr(self.alpha), _ptr(self.delta), self.ptr, self.width, col0,
-                L.LSP_MEM_DEVICE))
-        finally:
-            self.ctx.dev_free(da)
-            self.ctx.dev_free(db)
+        na, nb = len(pt.a), len(pt.b)
+        da = self._scratch
+        db = self._upload_cols(pt.a, n, da)
+        self._upload_cols(pt.b, n, db)
+        self.ctx._chk(L.lib().lsp_witness_permutation(
+            self.ctx.h, da, na, db, nb, n, _ptr(self.alpha), _ptr(self.delta), self.ptr, self.width, col0,
+            L.LSP_MEM_DEVICE))
         cfg = AirPermutationConfig(list(range(na)), list(range(na, na + nb)), na + nb, na + nb + 1)
         cfg.shift(col0)
         return cfg
@@ -186,18 +181,12 @@ class RawTrace:
         n = self.height
         lt.fill_filters()
         nt, nbc, na = len(lt.b), len(lt.b[0]), len(lt.a)
-        a = np.ascontiguousarray(np.stack([_pad(_col(c), n) for c in lt.a]))
-        b = np.ascontiguousarray(np.stack([_pad(_col(c), n) for t in lt.b for c in t]))
-        af = np.ascontiguousarray(_pad(lt.a_filter, n))
-        bf = np.ascontiguousarray(np.stack([_pad(f, n) for f in lt.b_filter]))
-        ptrs = [self._upload(x) for x in (a, b, af, bf)]
-        try:
-            self.ctx._chk(L.lib().lsp_witness_lookup(
-                self.ctx.h, ptrs[0], na, ptrs[1], nt, nbc, ptrs[2], ptrs[3], n, _ptr(self.alpha),
-                _ptr(self.delta), self.ptr, self.width, col0, L.LSP_MEM_DEVICE))
-        finally:
-            for p in ptrs:
-                self.ctx.dev_free(p)
+        ptrs = [self._scratch]
+        for cols in (lt.a, [c for t in lt.b for c in t], [lt.a_filter], list(lt.b_filter)):
+            ptrs.append(self._upload_cols(cols, n, ptrs[-1]))
+        self.ctx._chk(L.lib().lsp_witness_lookup(
+            self.ctx.h, ptrs[0], na, ptrs[1], nt, nbc, ptrs[2], ptrs[3], n, _ptr(self.alpha),
+            _ptr(self.delta), self.ptr, self.width, col0, L.LSP_MEM_DEVICE))
         # column ids (trace/src/lookup.rs:178-214)
         a_ids = list(range(na))
         b_ids = [[na + t * nbc + c for c in range(nbc)] for t in range(nt)]
@@ -210,10 +199,23 @@ class RawTrace:
         cfg.shift(col0)
         return cfg
 
-    def _upload(self, x: np.ndarray) -> int:
-        p = self.ctx.dev_alloc(max(x.nbytes, 32))
-        self.ctx.h2d(p, x)
-        return p
+    def _upload_cols(self, cols, n: int, p: int) -> int:
+        """len(cols) columns of n elements each, column-major at device address
+        p, each column straight from its own array (no stacked host copy); a
+        short column's tail is zeros (Vec::resize(n, [0u8; 32]):
+        trace/src/permutation.rs:134-140, trace/src/lookup.rs:231-245).
+        Returns the address after the last column."""
+        zeros = None
+        for k, c in enumerate(cols):
+            c = _col(c)
+            m = min(c.shape[0], n)
+            if m:
+                self.ctx.h2d(p + k * n * 32, c[:m])
+            if m < n:
+                if zeros is None or zeros.shape[0] < n - m:
+                    zeros = np.zeros((n - m, 4), np.uint64)
+                self.ctx.h2d(p + (k * n + m) * 32, zeros[:n - m])
+        return p + len(cols) * n * 32
 
     def get_trace(self, host: bool = False):
         """(device pointer, height, width), or the (height, width, 4) host matrix"""

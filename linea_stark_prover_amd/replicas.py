@@ -67,7 +67,29 @@ def init_from_env() -> Dist:
     import torch.distributed as dist
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
-    return Dist(rank, world, local, dist)
+    d = Dist(rank, world, local, dist)
+    share_host_cpus(d)
+    return d
+
+
+def share_host_cpus(d: Dist) -> Optional[int]:
+    """Size every rank's host pool from the ranks that really share its CPUs:
+    the ranks on this host with the same affinity set split it, a rank with a
+    set of its own keeps it (16 threads at most, as the library's default).
+    The library alone can only guess from LOCAL_WORLD_SIZE whether a small
+    set is shared or this rank's slice (host.cpp default_host_threads); here
+    the ranks compare their sets over the control group and export
+    LSP_HOST_THREADS before any context exists.  An LSP_HOST_THREADS the
+    caller set wins.  Returns the pool size chosen (None: left to the library)."""
+    if d.world <= 1 or "LSP_HOST_THREADS" in os.environ or not hasattr(os, "sched_getaffinity"):
+        return None
+    import socket
+    mask = tuple(sorted(os.sched_getaffinity(0)))
+    key = (socket.gethostname(), mask)
+    sharers = sum(1 for k in d.all_gather_object(key) if k == key)
+    n = max(1, min(16, len(mask) // max(sharers, 1)))
+    os.environ["LSP_HOST_THREADS"] = str(n)
+    return n
 
 
 def timed_steps(step: Callable[[], object], steps: int, warmup: int, d: Dist,

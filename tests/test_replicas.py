@@ -23,7 +23,9 @@ WORKER = textwrap.dedent("""
     # rank r sleeps (r+1)*20 ms per step: the reported time must be the slowest rank's
     el, _ = timed_steps(lambda: time.sleep(0.02 * (d.rank + 1)), 3, 1, d)
     print(json.dumps({{"rank": d.rank, "world": d.world, "elapsed": el,
-                       "trace_head": [int(x) for x in tr[0, 0]]}}), flush=True)
+                       "trace_head": [int(x) for x in tr[0, 0]],
+                       "host_threads": os.environ.get("LSP_HOST_THREADS"),
+                       "cpus": len(os.sched_getaffinity(0))}}), flush=True)
     d.close()
 """)
 
@@ -56,6 +58,8 @@ def test_two_rank_gloo_replicas(tmp_path, product_lib):
     assert [o["world"] for o in outs] == [2, 2]
     # max over ranks: both report the same elapsed, at least the slow rank's 3 x 40 ms
     assert abs(outs[0]["elapsed"] - outs[1]["elapsed"]) < 1e-9
+    # both ranks share this process's affinity set: each takes half of it (init_from_env)
+    assert [int(o["host_threads"]) for o in outs] == [max(1, min(16, o["cpus"] // 2)) for o in outs]
     assert outs[0]["elapsed"] >= 0.12
     # independent replicas: distinct traces per rank
     assert outs[0]["trace_head"] != outs[1]["trace_head"]
@@ -133,3 +137,40 @@ def test_bench_helpers():
     # a profile from another build is never used: null plus the reason
     bench.lde_traffic(5, 3)
     assert bench.TRAFFIC_SRC[(5, 3)].startswith("null")
+
+
+def test_host_pool_split_follows_affinity(tmp_path, product_lib):
+    """init_from_env sizes each rank's host pool from the ranks that share its
+    CPU set: ranks pinned to disjoint sets keep their own (no division), ranks
+    on one set split it"""
+    import json
+    cpus = sorted(os.sched_getaffinity(0))
+    if len(cpus) < 4:
+        pytest.skip("needs 4 CPUs")
+    half = len(cpus) // 2
+    worker = textwrap.dedent(f"""
+        import os, sys, json
+        sys.path.insert(0, {ROOT!r})
+        r = int(os.environ["RANK"])
+        cpus = {cpus!r}
+        os.sched_setaffinity(0, cpus[:{half}] if r == 0 else cpus[{half}:])
+        from linea_stark_prover_amd.replicas import init_from_env
+        d = init_from_env()
+        print(json.dumps({{"rank": d.rank, "threads": int(os.environ["LSP_HOST_THREADS"]),
+                           "cpus": len(os.sched_getaffinity(0))}}), flush=True)
+        d.close()
+    """)
+    script = tmp_path / "pin.py"
+    script.write_text(worker)
+    port = _free_port()
+    procs = [subprocess.Popen([sys.executable, str(script)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                              env=dict(os.environ, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE="2",
+                                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port)))
+             for r in range(2)]
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=240)
+        assert p.returncode == 0, e
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    for o in outs:  # disjoint sets: each rank's own, undivided
+        assert o["threads"] == min(16, o["cpus"]), o

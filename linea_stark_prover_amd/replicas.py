@@ -74,8 +74,9 @@ def init_from_env() -> Dist:
 
 def share_host_cpus(d: Dist) -> Optional[int]:
     """Size every rank's host pool from the ranks that really share its CPUs:
-    the ranks on this host with the same affinity set split it, a rank with a
-    set of its own keeps it (16 threads at most, as the library's default).
+    the ranks on this host under the same CPU quota, or with the same affinity
+    set, split it; a rank with a set of its own keeps it (16 threads at most,
+    as the library's default).
     The library alone can only guess from LOCAL_WORLD_SIZE whether a small
     set is shared or this rank's slice (host.cpp default_host_threads); here
     the ranks compare their sets over the control group and export
@@ -85,11 +86,44 @@ def share_host_cpus(d: Dist) -> Optional[int]:
         return None
     import socket
     mask = tuple(sorted(os.sched_getaffinity(0)))
-    key = (socket.gethostname(), mask)
+    quota = cgroup_cpu_quota()
+    if quota and quota < len(mask):
+        # a CPU quota (the GPU boxes: 16 CPUs' worth on a 256-CPU set) covers
+        # every rank of the cgroup: those on this host share it
+        key = (socket.gethostname(), "quota", quota)
+        avail = quota
+    else:
+        key = (socket.gethostname(), mask)
+        avail = len(mask)
     sharers = sum(1 for k in d.all_gather_object(key) if k == key)
-    n = max(1, min(16, len(mask) // max(sharers, 1)))
+    n = max(1, min(16, avail // max(sharers, 1)))
     os.environ["LSP_HOST_THREADS"] = str(n)
     return n
+
+
+def cgroup_cpu_quota() -> int:
+    """CPUs the cgroup's CPU quota allows, rounded up; 0 without a quota
+    (cgroup v2 cpu.max, v1 cpu.cfs_quota_us / cpu.cfs_period_us).  The GPU
+    boxes limit a job this way -- 16 CPUs' worth -- while its affinity set is
+    the whole 256-CPU machine, which the library's own default cannot tell
+    from a per-rank share."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q == "max":
+            return 0
+        q, per = float(q), float(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = float(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = float(f.read())
+        except (OSError, ValueError):
+            return 0
+    if q <= 0 or per <= 0:
+        return 0
+    return max(1, int(-(-q // per)))
 
 
 def timed_steps(step: Callable[[], object], steps: int, warmup: int, d: Dist,

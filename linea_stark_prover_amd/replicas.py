@@ -74,9 +74,12 @@ def init_from_env() -> Dist:
 
 def share_host_cpus(d: Dist) -> Optional[int]:
     """Size every rank's host pool from the ranks that really share its CPUs:
-    the ranks on this host under the same CPU quota, or with the same affinity
-    set, split it; a rank with a set of its own keeps it (16 threads at most,
-    as the library's default).
+    the ranks on this host with the same affinity set split it, a rank with a
+    set of its own keeps it (16 threads at most, as the library's default).
+    A cgroup CPU quota is not divided: eight ranks on one box's 16-CPU quota
+    proved faster with 16-thread pools each (8.65 M rows/s) than with strict
+    2-thread shares (8.26 M; profiles/r05r_*, r05z_*) -- the pools' work is
+    bursty latency chains that rarely coincide.
     The library alone can only guess from LOCAL_WORLD_SIZE whether a small
     set is shared or this rank's slice (host.cpp default_host_threads); here
     the ranks compare their sets over the control group and export
@@ -86,70 +89,8 @@ def share_host_cpus(d: Dist) -> Optional[int]:
         return None
     import socket
     mask = tuple(sorted(os.sched_getaffinity(0)))
-    quota = cgroup_cpu_quota()
-    if quota and quota < len(mask):
-        # a CPU quota (the GPU boxes: 16 CPUs' worth on a 256-CPU set) covers
-        # every rank of the cgroup: those on this host share it
-        key = (socket.gethostname(), "quota", quota)
-        avail = quota
-    else:
-        key = (socket.gethostname(), mask)
-        avail = len(mask)
+    key = (socket.gethostname(), mask)
     sharers = sum(1 for k in d.all_gather_object(key) if k == key)
-    n = max(1, min(16, avail // max(sharers, 1)))
+    n = max(1, min(16, len(mask) // max(sharers, 1)))
     os.environ["LSP_HOST_THREADS"] = str(n)
     return n
-
-
-def cgroup_cpu_quota() -> int:
-    """CPUs the cgroup's CPU quota allows, rounded up; 0 without a quota
-    (cgroup v2 cpu.max, v1 cpu.cfs_quota_us / cpu.cfs_period_us).  The GPU
-    boxes limit a job this way -- 16 CPUs' worth -- while its affinity set is
-    the whole 256-CPU machine, which the library's own default cannot tell
-    from a per-rank share."""
-    try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
-            q, per = f.read().split()[:2]
-        if q == "max":
-            return 0
-        q, per = float(q), float(per)
-    except (OSError, ValueError):
-        try:
-            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
-                q = float(f.read())
-            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
-                per = float(f.read())
-        except (OSError, ValueError):
-            return 0
-    if q <= 0 or per <= 0:
-        return 0
-    return max(1, int(-(-q // per)))
-
-
-def timed_steps(step: Callable[[], object], steps: int, warmup: int, d: Dist,
-                sync: Callable[[], None] = lambda: None, on_step: Callable[[], None] = lambda: None,
-                step_times: Optional[list] = None):
-    """W untimed steps, barrier + sync, K timed steps, sync + barrier; returns
-    (max-over-ranks elapsed seconds, last step result).  `step_times` (if given)
-    receives this rank's wall time of every timed step (the step itself
-    returns with its result on the host)."""
-    out = None
-    for _ in range(warmup):
-        out = step()
-    d.barrier()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        ts = time.perf_counter()
-        out = step()
-        if step_times is not None:
-            step_times.append(time.perf_counter() - ts)
-        on_step()
-    sync()
-    d.barrier()
-    return d.max(time.perf_counter() - t0), out
-
-
-def rank_seed(base_seed: int, rank: int) -> int:
-    """Each replica proves a distinct synthetic trace."""
-    return base_seed + rank

@@ -94,3 +94,32 @@ def share_host_cpus(d: Dist) -> Optional[int]:
     n = max(1, min(16, len(mask) // max(sharers, 1)))
     os.environ["LSP_HOST_THREADS"] = str(n)
     return n
+
+
+def timed_steps(step: Callable[[], object], steps: int, warmup: int, d: Dist,
+                sync: Callable[[], None] = lambda: None, on_step: Callable[[], None] = lambda: None,
+                step_times: Optional[list] = None):
+    """W untimed steps, barrier + sync, K timed steps, sync + barrier; returns
+    (max-over-ranks elapsed seconds, last step result).  `step_times` (if given)
+    receives this rank's wall time of every timed step (the step itself
+    returns with its result on the host)."""
+    out = None
+    for _ in range(warmup):
+        out = step()
+    d.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ts = time.perf_counter()
+        out = step()
+        if step_times is not None:
+            step_times.append(time.perf_counter() - ts)
+        on_step()
+    sync()
+    d.barrier()
+    return d.max(time.perf_counter() - t0), out
+
+
+def rank_seed(base_seed: int, rank: int) -> int:
+    """Each replica proves a distinct synthetic trace."""
+    return base_seed + rank

@@ -77,9 +77,9 @@ def share_host_cpus(d: Dist) -> Optional[int]:
     the ranks on this host with the same affinity set split it, a rank with a
     set of its own keeps it (16 threads at most, as the library's default).
     A cgroup CPU quota is not divided: eight ranks on one box's 16-CPU quota
-    proved faster with 16-thread pools each (8.65 M rows/s) than with strict
-    2-thread shares (8.26 M; profiles/r05r_*, r05z_*) -- the pools' work is
-    bursty latency chains that rarely coincide.
+    ran no faster with strict 2-thread shares (8.26 M rows/s) than with
+    16-thread pools each (8.40-8.65 M; profiles/r05r_*, r05z*_*) -- the
+    pools' work is bursty latency chains that rarely coincide.
     The library alone can only guess from LOCAL_WORLD_SIZE whether a small
     set is shared or this rank's slice (host.cpp default_host_threads); here
     the ranks compare their sets over the control group and export

@@ -418,6 +418,8 @@ def main_leg(args, dist, ranks_seen):
         if world == 1 and not shard and not args.no_host_trace_leg:
             out["prove_time_host_trace_s"] = host_trace_leg(args, ctx, trace, air, pub)
             out["rows_per_s_host_trace"] = h / out["prove_time_host_trace_s"]["median"]
+            if args.inflight > 1:
+                out["inflight_host_trace"] = inflight(args, cfg, air, pub, trace, ctx, dtrace, host=True)
     ctx.dev_free(dtrace)
     return out, ctx
 
@@ -762,12 +764,15 @@ def collective_table(ctx, dist):
             "comm_init_ms_by_rank": [round(i, 3) for _, i in logs]}
 
 
-def inflight(args, cfg, air, pub, trace, ctx, dtrace):
+def inflight(args, cfg, air, pub, trace, ctx, dtrace, host=False):
     """Production throughput mode: P independent proofs in flight on one GPU
     (P contexts = P HIP streams, one host thread each), so one proof's
     latency-bound phases (narrow Merkle levels, transcript, tree tops) overlap
-    another's hashing.  Reported beside `value` (the sequential single-proof
-    rate), never instead of it."""
+    another's hashing.  host=True: every proof starts from the trace in host
+    memory (the drop-in prove(RowMajorMatrix)), so one context's PCIe upload
+    overlaps the others' compute instead of preceding its own proof.
+    Reported beside `value` (the sequential single-proof rate), never instead
+    of it."""
     from linea_stark_prover_amd.prover import Context
     P, K = args.inflight, max(args.steps, 2)
     h, w = trace.shape[0], trace.shape[1]
@@ -785,7 +790,10 @@ def inflight(args, cfg, air, pub, trace, ctx, dtrace):
 
     def worker(i):
         for _ in range(K):
-            ctxs[i].prove(ptrs[i], air, pub, h, w)
+            if host:
+                ctxs[i].prove(trace, air, pub)
+            else:
+                ctxs[i].prove(ptrs[i], air, pub, h, w)
 
     t = time.perf_counter()
     th = [threading.Thread(target=worker, args=(i,)) for i in range(P)]
@@ -799,7 +807,9 @@ def inflight(args, cfg, air, pub, trace, ctx, dtrace):
         c.close()
     return {"proofs_in_flight": P, "proofs": P * K, "value": P * K * h / dt, "unit": "trace-rows/s",
             "ms_per_proof": dt / (P * K) * 1e3,
-            "note": "independent proofs on P streams of one GPU; value above is one proof at a time"}
+            "note": ("independent proofs on P streams of one GPU, each trace uploaded from pageable host memory "
+                     "inside its proof" if host else "independent proofs on P streams of one GPU") +
+                    "; value above is one proof at a time"}
 
 
 NTT_MADS_PER_PRODUCT = 162  # the NTT's 29-bit-limb product: 81 limb products + 81 reduction MADs

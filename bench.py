@@ -780,9 +780,13 @@ def inflight(args, cfg, air, pub, trace, ctx, dtrace, host=False):
     for _ in range(P - 1):
         c = Context(cfg, device=ctx.device)
         c.set_phase_timing(True, only=ROOFLINE_PHASES)
-        p = c.dev_alloc(trace.nbytes)
-        c.h2d(p, trace)
-        c.prove(p, air, pub, h, w)  # warm
+        if host:
+            p = None
+            c.prove(trace, air, pub)  # warm
+        else:
+            p = c.dev_alloc(trace.nbytes)
+            c.h2d(p, trace)
+            c.prove(p, air, pub, h, w)  # warm
         ctxs.append(c)
         ptrs.append(p)
     for c in ctxs:
@@ -803,7 +807,8 @@ def inflight(args, cfg, air, pub, trace, ctx, dtrace, host=False):
         x.join()
     dt = time.perf_counter() - t
     for c, p in zip(ctxs[1:], ptrs[1:]):
-        c.dev_free(p)
+        if p is not None:
+            c.dev_free(p)
         c.close()
     return {"proofs_in_flight": P, "proofs": P * K, "value": P * K * h / dt, "unit": "trace-rows/s",
             "ms_per_proof": dt / (P * K) * 1e3,

@@ -72,6 +72,124 @@ MAD_PER_FR_MUL = 128        # 8 x 32-bit limbs: 64 product + 64 reduction MADs (
 FRMUL_PEAK_GPS = SIMDS * 64 / 4 * NOMINAL_GHZ / MAD_PER_FR_MUL  # 307.2 G Fr-mul/s (v_mad_u64_u32: 4 cycles)
 
 
+class ClockSampler:
+    """The engine clock the SMU reports while the timed steps run (VERDICT r5
+    item 1: a box-speed stamp, so lines from different boxes can be told
+    apart from code changes).  A thread reads amdsmi's gpu_metrics every
+    `period` s between start() and stop(): current_gfxclk(s) (per XCD on
+    MI355X; their mean), average_gfxclk_frequency and socket power.  Read-only
+    sysfs queries; the device is matched by PCI bus id.  Absent amdsmi or a
+    device it cannot see, `status` says why and summary() is None."""
+
+    def __init__(self, hip_device: int, period: float = 0.02):
+        self.period, self.samples, self.handle, self.bdf = period, [], None, None
+        self.status, self._stop, self._th = "ok", threading.Event(), None
+        try:
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            buf = ctypes.create_string_buffer(64)
+            if hip.hipDeviceGetPCIBusId(buf, 64, ctypes.c_int(hip_device)) != 0:
+                raise RuntimeError("hipDeviceGetPCIBusId failed")
+            self.bdf = buf.value.decode().lower()
+            import amdsmi
+            amdsmi.amdsmi_init()
+            handles = amdsmi.amdsmi_get_processor_handles()
+            for hd in handles:
+                if amdsmi.amdsmi_get_gpu_device_bdf(hd).lower() == self.bdf:
+                    self.handle = hd
+            if self.handle is None and len(handles) == 1:
+                self.handle = handles[0]
+            if self.handle is None:
+                self.status = f"no amdsmi device with bus id {self.bdf} among {len(handles)}"
+            else:
+                self._read()  # fails here, not in the thread
+        except Exception as e:  # noqa: BLE001  (a stamp, never a reason to fail the bench)
+            self.status, self.handle = f"{type(e).__name__}: {e}", None
+
+    def _read(self):
+        import amdsmi
+        m = amdsmi.amdsmi_get_gpu_metrics_info(self.handle)
+        clks = m.get("current_gfxclks")
+        clks = [c for c in clks if isinstance(c, (int, float)) and c > 0] if isinstance(clks, list) else []
+        cur = statistics.mean(clks) if clks else m.get("current_gfxclk")
+        num = lambda v: float(v) if isinstance(v, (int, float)) else None  # noqa: E731
+        return (num(cur), num(m.get("average_gfxclk_frequency")), num(m.get("current_socket_power")))
+
+    def _run(self):
+        while not self._stop.wait(self.period):
+            try:
+                self.samples.append(self._read())
+            except Exception:  # noqa: BLE001
+                pass
+
+    def start(self):
+        if self.handle is not None:
+            self.samples, self._stop = [], threading.Event()
+            self._th = threading.Thread(target=self._run, daemon=True)
+            self._th.start()
+        return self
+
+    def stop(self):
+        if self._th is not None:
+            self._stop.set()
+            self._th.join()
+            self._th = None
+        return self.summary()
+
+    def summary(self):
+        cur = [s[0] for s in self.samples if s[0]]
+        if not cur:
+            return None
+        avg = [s[1] for s in self.samples if s[1]]
+        pw = [s[2] for s in self.samples if s[2]]
+        return {"sclk_mhz_mean": statistics.mean(cur), "sclk_mhz_median": statistics.median(cur),
+                "sclk_mhz_min": min(cur), "sclk_mhz_max": max(cur),
+                "avg_gfxclk_mhz_mean": statistics.mean(avg) if avg else None,
+                "socket_power_w_mean": statistics.mean(pw) if pw else None,
+                "samples": len(cur), "period_s": self.period}
+
+
+# The box that benched the round-5 final library at 60.67 ms (profiles/r05final2_bench.json)
+# and the driver's round-5 box (BENCH_r05.json, 63.35 ms): the probes there, for scale.
+BOX_REFERENCE = {"source": "profiles/r06a_box_speed.json"}
+
+
+def box_speed(ctx, sclk, status, ms_per_step):
+    """What this box did while the line was measured, beside the line: the
+    engine clock during the timed steps (ClockSampler), the GPU's
+    full-occupancy Poseidon2 rate (k_calib_perm, best of 2..32 waves per SIMD)
+    and one host thread's Poseidon2 compression rate (the tree tops' and FRI
+    tail's path).  Lines from two boxes compare by these, not by assumption."""
+    out = {"gpu_perm_mperm_per_s": ctx.calibrate_poseidon2(),
+           "gpu_perm_note": "k_calib_perm over 2..32 waves per SIMD (best): a full-occupancy throughput probe "
+                            "of the permutation every Merkle kernel runs",
+           "host_compress_k_per_s": host_compress_rate(ctx) / 1e3,
+           "host_compress_note": "lsp_host_compress_batch, one thread, 4096 compressions, best of 5",
+           "sclk_during_timed_steps": sclk, "sclk_status": status}
+    if sclk:
+        out["ms_per_step_x_sclk_ghz"] = ms_per_step * sclk["sclk_mhz_mean"] / 1e3
+    return out
+
+
+def host_compress_rate(ctx, n: int = 4096, reps: int = 5) -> float:
+    """Host Poseidon2 compressions per second on one thread (lsp_host_compress_batch:
+    the IFMA path the tree tops and the FRI tail run on), best of `reps`: the
+    host half of the box-speed stamp."""
+    import ctypes
+    import numpy as np
+    from linea_stark_prover_amd import _lib
+    rng = np.random.default_rng(7)
+    pairs = np.ascontiguousarray(rng.integers(0, 1 << 60, size=(2 * n, 4), dtype=np.uint64))  # < 2^252 < r
+    out = np.zeros((n, 4), dtype=np.uint64)
+    best = 0.0
+    for _ in range(reps):
+        t = time.perf_counter()
+        _lib.check(_lib.lib().lsp_host_compress_batch(ctx.h, pairs.ctypes.data_as(_lib.c_fr_p), n,
+                                                      out.ctypes.data_as(_lib.c_fr_p)))
+        best = max(best, n / (time.perf_counter() - t))
+    return best
+
+
 def _lib_src() -> str:
     """the stamp of the library being benched (build.library_hash); the
     working tree's hash only for an unstamped library"""
@@ -289,7 +407,10 @@ def main_leg(args, dist, ranks_seen):
         step = lambda: S.prove_sharded(ctx, dtrace, air, pub, h, w)  # noqa: E731
     else:
         step = lambda: ctx.prove(dtrace, air, pub, h, w)  # noqa: E731
-    elapsed, proof = timed_steps(step, args.steps, args.warmup, dist, sync=ctx.synchronize, step_times=step_s)
+    clocks = ClockSampler(ctx.device)
+    elapsed, proof = timed_steps(step, args.steps, args.warmup, dist, sync=ctx.synchronize, step_times=step_s,
+                                 on_start=clocks.start)
+    sclk = clocks.stop()
     # the last timed step's LDE and Merkle times (HIP events on the prover's
     # stream, inside the timed region): the library resolves its phase events
     # lazily, so reading them after every step would put that inside the timing
@@ -409,6 +530,7 @@ def main_leg(args, dist, ranks_seen):
                               "valu_issue_source": VALU_SRC.get("src"),
                               "perms": trace_perms, "fr_mul_per_perm": FR_MUL_PER_PERM, "ms": merkle_ms},
         }
+        out["box_speed"] = box_speed(ctx, sclk, clocks.status, ms_per_step)
         if table is not None:
             out.update(table)
         if shard and world > 1:

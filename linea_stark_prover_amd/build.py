@@ -61,11 +61,7 @@ def library_hash() -> str | None:
     to the library at link time), or None when the library has no stamp.  The
     stamp travels with the library, so a profile taken on a GPU box names the
     build that ran there even when the working tree has moved on."""
-    try:
-        with open(STAMP) as fh:
-            return fh.read().strip() or None
-    except OSError:
-        return None
+    return _read_stamp(LIB)
 
 
 def _headers():
@@ -84,6 +80,18 @@ DBG_BUILD = os.path.join(PKG, "_build_dbg")
 DBG_LIB = os.path.join(LIBDIR, "liblsp_hip_dbg.so")
 
 
+def _stamp_path(lib):
+    return lib + ".src"
+
+
+def _read_stamp(lib):
+    try:
+        with open(_stamp_path(lib)) as fh:
+            return fh.read().strip() or None
+    except OSError:
+        return None
+
+
 def _compile(src, build_dir=BUILD, extra=()):
     obj = os.path.join(build_dir, os.path.splitext(src)[0] + ".o")
     flags = CFLAGS + list(extra)
@@ -97,10 +105,22 @@ def _compile(src, build_dir=BUILD, extra=()):
 
 
 def build(force: bool = False, jobs: int = None, verbose: bool = True, debug_bounds: bool = False) -> str:
+    """Compile what is stale and relink.  The stamp next to the library names
+    the sources it was linked from; a library whose stamp differs from the
+    current sources is rebuilt from scratch, never relabelled: a checkout or an
+    ``rsync -t`` can change a source without making it newer than its object,
+    and a relabelled stale library would tie profiles to code it does not run
+    (VERDICT r5 item 5)."""
     build_dir, lib = (DBG_BUILD, DBG_LIB) if debug_bounds else (BUILD, LIB)
     extra = ["-DLSP_DEBUG_BOUNDS"] if debug_bounds else []
     os.makedirs(build_dir, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
+    want = source_hash()
+    if not force and _read_stamp(lib) != want:
+        force = True
+        if verbose and os.path.exists(lib):
+            print(f"[lsp build] {os.path.basename(lib)} stamp {_read_stamp(lib)} != sources {want}: full rebuild",
+                  flush=True)
     hdrs = _headers()
     todo = []
     objs = []
@@ -123,9 +143,9 @@ def build(force: bool = False, jobs: int = None, verbose: bool = True, debug_bou
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         if verbose:
             print(f"[lsp build] linked {lib}", flush=True)
-    if not debug_bounds and library_hash() != source_hash():
-        with open(STAMP, "w") as fh:
-            fh.write(source_hash() + "\n")
+        # the stamp is written only here, after a link from the sources it names
+        with open(_stamp_path(lib), "w") as fh:
+            fh.write(want + "\n")
     return lib
 
 

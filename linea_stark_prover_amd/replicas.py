@@ -85,12 +85,18 @@ def share_host_cpus(d: Dist) -> Optional[int]:
     the ranks compare their sets over the control group and export
     LSP_HOST_THREADS before any context exists.  An LSP_HOST_THREADS the
     caller set wins.  Returns the pool size chosen (None: left to the library)."""
-    if d.world <= 1 or "LSP_HOST_THREADS" in os.environ or not hasattr(os, "sched_getaffinity"):
+    if d.world <= 1:
         return None
+    # every rank takes part in the collective, whatever its own environment
+    # says: a rank that skipped it (its own LSP_HOST_THREADS set) would leave
+    # the others blocked in the gloo all_gather (ADVICE r5)
     import socket
-    mask = tuple(sorted(os.sched_getaffinity(0)))
+    mask = tuple(sorted(os.sched_getaffinity(0))) if hasattr(os, "sched_getaffinity") else None
     key = (socket.gethostname(), mask)
-    sharers = sum(1 for k in d.all_gather_object(key) if k == key)
+    keys = d.all_gather_object(key)
+    if "LSP_HOST_THREADS" in os.environ or mask is None:
+        return None
+    sharers = sum(1 for k in keys if k == key)
     n = max(1, min(16, len(mask) // max(sharers, 1)))
     os.environ["LSP_HOST_THREADS"] = str(n)
     return n
@@ -98,16 +104,19 @@ def share_host_cpus(d: Dist) -> Optional[int]:
 
 def timed_steps(step: Callable[[], object], steps: int, warmup: int, d: Dist,
                 sync: Callable[[], None] = lambda: None, on_step: Callable[[], None] = lambda: None,
-                step_times: Optional[list] = None):
+                step_times: Optional[list] = None, on_start: Callable[[], object] = lambda: None):
     """W untimed steps, barrier + sync, K timed steps, sync + barrier; returns
     (max-over-ranks elapsed seconds, last step result).  `step_times` (if given)
     receives this rank's wall time of every timed step (the step itself
-    returns with its result on the host)."""
+    returns with its result on the host).  `on_start` runs once after the
+    opening barrier + sync, just before the clock starts (bench.py's clock
+    sampler)."""
     out = None
     for _ in range(warmup):
         out = step()
     d.barrier()
     sync()
+    on_start()
     t0 = time.perf_counter()
     for _ in range(steps):
         ts = time.perf_counter()

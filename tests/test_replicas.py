@@ -174,3 +174,37 @@ def test_host_pool_split_follows_affinity(tmp_path, product_lib):
         outs.append(json.loads(o.strip().splitlines()[-1]))
     for o in outs:  # disjoint sets: each rank's own, undivided
         assert o["threads"] == min(16, o["cpus"]), o
+
+
+def test_host_pool_mixed_override_does_not_hang(tmp_path, product_lib):
+    """a rank with its own LSP_HOST_THREADS still joins the control
+    group's all_gather, so ranks without it do not block; its override wins"""
+    import json
+    worker = textwrap.dedent(f"""
+        import os, sys, json
+        sys.path.insert(0, {ROOT!r})
+        from linea_stark_prover_amd.replicas import init_from_env
+        d = init_from_env()
+        print(json.dumps({{"rank": d.rank, "threads": int(os.environ["LSP_HOST_THREADS"])}}), flush=True)
+        d.close()
+    """)
+    script = tmp_path / "mixed.py"
+    script.write_text(worker)
+    port = _free_port()
+    base = {k: v for k, v in os.environ.items() if k != "LSP_HOST_THREADS"}
+    procs = []
+    for r in range(2):
+        env = dict(base, WORLD_SIZE="2", RANK=str(r), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if r == 1:
+            env["LSP_HOST_THREADS"] = "3"
+        procs.append(subprocess.Popen([sys.executable, str(script)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      text=True, env=env))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=240)
+        assert p.returncode == 0, e
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    outs.sort(key=lambda o: o["rank"])
+    assert outs[1]["threads"] == 3
+    assert 1 <= outs[0]["threads"] <= 16

@@ -149,9 +149,6 @@ class ClockSampler:
                 "samples": len(cur), "period_s": self.period}
 
 
-# The box that benched the round-5 final library at 60.67 ms (profiles/r05final2_bench.json)
-# and the driver's round-5 box (BENCH_r05.json, 63.35 ms): the probes there, for scale.
-BOX_REFERENCE = {"source": "profiles/r06a_box_speed.json"}
 
 
 def box_speed(ctx, sclk, status, ms_per_step):

@@ -350,10 +350,25 @@ int lsp_comm_selftest(lsp_ctx *ctx);
  * in the environment forces the choice. */
 int lsp_comm_exchange_plan(lsp_ctx *ctx, size_t h, size_t w, size_t q, double *allgather_gbs, double *intt_gelem_s,
                            size_t *probe_bytes, int *split, double *allgather_ms, double *redundant_ms);
+/* every rank's own calibration probes, rank order, 3 doubles per rank:
+ * allgather GB/s of the 4 MiB probe, of the 256 MiB probe (0: not run, the
+ * small one was below 20 GB/s on some rank), inverse-NTT G elements/s on
+ * random data -- the raw values whose minimum lsp_comm_exchange_plan uses.
+ * *n = 3 x ranks (0 when never calibrated); out == NULL or cap < *n -> only *n */
+int lsp_comm_calibration(lsp_ctx *ctx, double *per_rank, size_t cap, size_t *n);
+/* the quotient-chunk broadcasts a sharded proof of h rows with q chunks
+ * issues on ctx's communicator (either inverse-NTT exchange): how many, the
+ * bytes of each, and their total time at the calibrated allgather bandwidth
+ * (0 when uncalibrated); at 2^26 rows over 8 ranks: 4 x 2 GiB.  Any output
+ * may be NULL. */
+int lsp_comm_quotient_exchange(lsp_ctx *ctx, size_t h, size_t q, size_t *bcasts, size_t *bytes_each,
+                               double *model_ms);
 /* threads of ctx's host pool (tree tops, FRI tail, query assembly): up to 16,
- * from this process's CPU affinity set -- divided among LOCAL_WORLD_SIZE
- * ranks only when that set is the machine's or holds >= 16 CPUs per rank
- * (else it is taken as this rank's own slice); LSP_HOST_THREADS overrides */
+ * from this process's CPU affinity set divided among LOCAL_WORLD_SIZE ranks
+ * (the library cannot tell a set the ranks share from a slice pinned for this
+ * rank alone, and divides).  LSP_HOST_THREADS overrides: a launcher that pins
+ * each rank to CPUs of its own sets it (the Python launch path,
+ * replicas.init_from_env, compares the ranks' sets and sets it exactly) */
 int lsp_ctx_host_threads(lsp_ctx *ctx, int *n);
 /* rank and size of the attached communicator (LSP_E_STATE if none) */
 int lsp_comm_info(lsp_ctx *ctx, int *rank, int *size);
@@ -495,6 +510,12 @@ int lsp_calibrate_fr_mul(lsp_ctx *ctx, double *gmul_per_s);
  * the device permutation kernels' code): the peak the Merkle kernels'
  * roofline (bench.py roofline_valu) is quoted against, in M perm/s. */
 int lsp_calibrate_poseidon2(lsp_ctx *ctx, double *mperm_per_s);
+/* this GPU's inverse-NTT rate in G elements/s on an h x w matrix of seeded
+ * random field elements (h = 2^log_h): the median of 5 timed inverse NTTs
+ * after a warm-up, the probe lsp_comm_selftest calibrates the exchange with
+ * (log_h 20, w 8) -- random operands, not zeros, since this chip is
+ * power-held on MAD-dense work */
+int lsp_calibrate_intt(lsp_ctx *ctx, uint32_t log_h, size_t w, double *gelem_per_s);
 
 /* ------------------------------------------------------------- witness */
 /* Synthetic permutation trace with the witness columns of

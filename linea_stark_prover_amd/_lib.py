@@ -129,6 +129,11 @@ _SIGS = {
     "lsp_ctx_set_phase_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                                 ctypes.c_size_t]),
     "lsp_comm_selftest": (ctypes.c_int, [ctypes.c_void_p]),
+    "lsp_comm_calibration": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t,
+                                            ctypes.POINTER(ctypes.c_size_t)]),
+    "lsp_comm_quotient_exchange": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                                  ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t),
+                                                  ctypes.POINTER(ctypes.c_double)]),
     "lsp_comm_exchange_plan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                               ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_int),
@@ -177,6 +182,8 @@ _SIGS = {
                                           ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]),
     "lsp_raw_trace_free": (ctypes.c_int, [ctypes.c_void_p]),
     "lsp_calibrate_poseidon2": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
+    "lsp_calibrate_intt": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_size_t,
+                                          ctypes.POINTER(ctypes.c_double)]),
     "lsp_gen_permutation_trace": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, c_fr_p, c_fr_p,
                                                  ctypes.c_int, c_fr_p]),
     "lsp_gen_permutation_trace_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
@@ -196,8 +203,13 @@ def lib() -> ctypes.CDLL:
             raise ImportError(f"liblsp_hip.so not found at {LIB_PATH}; run "
                               "`python -m linea_stark_prover_amd.build` (no CPU fallback exists)")
         L = ctypes.CDLL(LIB_PATH)
+        # an older build chosen for an A/B (LSP_LIB_OLDER=1 beside LSP_LIB) may
+        # lack later entry points; the product library must export them all
+        older = os.environ.get("LSP_LIB_OLDER") == "1"
         for name, (res, args) in _SIGS.items():
-            f = getattr(L, name)
+            f = getattr(L, name, None) if older else getattr(L, name)
+            if f is None:
+                continue
             f.restype = res
             f.argtypes = args
         _lib = L

@@ -69,13 +69,6 @@ def _headers():
         [os.path.join(ROOT, "include", "lsp.h")]
 
 
-def _stale(target, deps):
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
-
-
 DBG_BUILD = os.path.join(PKG, "_build_dbg")
 DBG_LIB = os.path.join(LIBDIR, "liblsp_hip_dbg.so")
 
@@ -104,46 +97,63 @@ def _compile(src, build_dir=BUILD, extra=()):
     return obj
 
 
+def _file_hash(path, seed=b""):
+    import hashlib
+    h = hashlib.sha256(seed)
+    with open(path, "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def build(force: bool = False, jobs: int = None, verbose: bool = True, debug_bounds: bool = False) -> str:
-    """Compile what is stale and relink.  The stamp next to the library names
-    the sources it was linked from; a library whose stamp differs from the
-    current sources is rebuilt from scratch, never relabelled: a checkout or an
-    ``rsync -t`` can change a source without making it newer than its object,
-    and a relabelled stale library would tie profiles to code it does not run
-    (VERDICT r5 item 5)."""
+    """Compile what changed and relink.  "Changed" is decided by content, not
+    mtimes: every object carries the hash of its source, the headers and the
+    flags it was compiled from (``x.o.src``), and the library the hash of
+    everything it was linked from (``liblsp_hip.so.src``, the stamp bench.py
+    ties profiles to).  A checkout or an ``rsync -t`` can change a source
+    without making it newer than its object; that object is recompiled and the
+    library relinked, never relabelled."""
+    import hashlib
     build_dir, lib = (DBG_BUILD, DBG_LIB) if debug_bounds else (BUILD, LIB)
     extra = ["-DLSP_DEBUG_BOUNDS"] if debug_bounds else []
     os.makedirs(build_dir, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     want = source_hash()
-    if not force and _read_stamp(lib) != want:
-        force = True
-        if verbose and os.path.exists(lib):
-            print(f"[lsp build] {os.path.basename(lib)} stamp {_read_stamp(lib)} != sources {want}: full rebuild",
-                  flush=True)
-    hdrs = _headers()
-    todo = []
-    objs = []
+    common = hashlib.sha256(" ".join(CFLAGS + extra + [ARCH]).encode())
+    for hdr in sorted(_headers()):
+        common.update(os.path.basename(hdr).encode())
+        with open(hdr, "rb") as fh:
+            common.update(fh.read())
+    seed = common.digest()
+    todo, objs, hashes = [], [], {}
     for s in SOURCES:
         obj = os.path.join(build_dir, os.path.splitext(s)[0] + ".o")
         objs.append(obj)
-        if force or _stale(obj, [os.path.join(CSRC, s)] + hdrs):
+        hashes[s] = _file_hash(os.path.join(CSRC, s), seed)
+        if force or not os.path.exists(obj) or _read_stamp(obj) != hashes[s]:
             todo.append(s)
     jobs = jobs or min(len(todo) or 1, os.cpu_count() or 4, 16)
     if todo:
         if verbose:
             print(f"[lsp build] compiling {len(todo)} file(s) for {ARCH}{' (debug-bounds)' if debug_bounds else ''}: "
                   f"{' '.join(todo)}", flush=True)
+
+        def one(src):
+            obj = _compile(src, build_dir, extra)
+            with open(_stamp_path(obj), "w") as fh:
+                fh.write(hashes[src] + "\n")
+
         with cf.ThreadPoolExecutor(jobs) as ex:
-            list(ex.map(lambda src: _compile(src, build_dir, extra), todo))
-    if todo or _stale(lib, objs):
+            list(ex.map(one, todo))
+    if todo or not os.path.exists(lib) or _read_stamp(lib) != want:
         cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", lib] + objs + ["-lpthread", "-ldl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         if verbose:
             print(f"[lsp build] linked {lib}", flush=True)
-        # the stamp is written only here, after a link from the sources it names
+        # the stamp is written only here, after a link from objects whose own
+        # stamps name the sources they were compiled from
         with open(_stamp_path(lib), "w") as fh:
             fh.write(want + "\n")
     return lib

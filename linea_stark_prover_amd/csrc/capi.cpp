@@ -1011,6 +1011,32 @@ int lsp_comm_exchange_plan(lsp_ctx* ctx, size_t h, size_t w, size_t q, double* a
     });
 }
 
+int lsp_comm_calibration(lsp_ctx* ctx, double* per_rank, size_t cap, size_t* n) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && n, LSP_E_ARG, "null argument");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        LSP_REQUIRE(ctx->comm, LSP_E_STATE, "no communicator attached");
+        const std::vector<double>& raw = ctx->comm->calib_raw;
+        *n = raw.size();
+        if (per_rank && cap >= raw.size()) std::copy(raw.begin(), raw.end(), per_rank);
+    });
+}
+
+int lsp_comm_quotient_exchange(lsp_ctx* ctx, size_t h, size_t q, size_t* bcasts, size_t* bytes_each,
+                               double* model_ms) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx, LSP_E_ARG, "null ctx");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        LSP_REQUIRE(ctx->comm, LSP_E_STATE, "no communicator attached");
+        LSP_REQUIRE(q == 0 || (q & (q - 1)) == 0, LSP_E_ARG, "q must be 0 or a power of two");
+        LSP_REQUIRE(h >= 2 && (h & (h - 1)) == 0, LSP_E_ARG, "h must be a power of two >= 2");
+        const QuotientExchange x = quotient_exchange(*ctx->comm, h, q, ctx->log_blowup);
+        if (bcasts) *bcasts = x.bcasts;
+        if (bytes_each) *bytes_each = x.bytes_each;
+        if (model_ms) *model_ms = x.model_ms;
+    });
+}
+
 int lsp_ctx_host_threads(lsp_ctx* ctx, int* n) {
     return guarded(ctx, [&] {
         LSP_REQUIRE(ctx && n, LSP_E_ARG, "null argument");
@@ -1363,6 +1389,17 @@ int lsp_calibrate_poseidon2(lsp_ctx* ctx, double* mperm_per_s) {
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
         *mperm_per_s = best;
+    });
+}
+
+int lsp_calibrate_intt(lsp_ctx* ctx, uint32_t log_h, size_t w, double* gelem_per_s) {
+    return guarded(ctx, [&] {
+        LSP_REQUIRE(ctx && gelem_per_s, LSP_E_ARG, "null argument");
+        LSP_REQUIRE(log_h >= 1 && log_h <= 26 && w >= 1 && w <= 1024, LSP_E_ARG, "bad inverse-NTT probe shape");
+        std::lock_guard<std::mutex> g(ctx->mu);
+        need_gpu(ctx);
+        *gelem_per_s = calibrate_intt(ctx, log_h, w, 5, nullptr);
+        ctx->release("calib_intt_");
     });
 }
 

@@ -51,6 +51,11 @@ struct Comm {
     // 0 = not measured (then the split inverse is the default).
     double ag_gbs = 0, intt_gelem_s = 0;
     size_t ag_probe_bytes = 0;
+    // every rank's own probe results, rank order, 3 per rank: allgather GB/s of
+    // the 4 MiB probe, of the 256 MiB probe (0: not run), inverse-NTT G
+    // elements/s (lsp_comm_calibration) -- so a biased minimum can be seen
+    std::vector<double> calib_raw;
+    std::string calib_status = "not calibrated";
     virtual ~Comm() {
         for (CommRec& r : log) {
             if (r.e0) (void)hipEventDestroy(r.e0);

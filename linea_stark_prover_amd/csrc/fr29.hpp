@@ -195,8 +195,12 @@ __device__ __forceinline__ F29 f29_reduce(const F29& a) {
 // normalised and < 2 r (the same value f29_reduce returns).
 constexpr uint32_t F29_QTAB_N = 64;
 
-// fill the table (F29_QTAB_N entries of 3 x uint4: limbs 0-3, 4-7, 8); the
-// caller's next __syncthreads publishes it
+// fill the table (F29_QTAB_N entries in three planes: limbs 0-3 at t[q], limbs
+// 4-7 at t[F29_QTAB_N + q], limb 8 at ((uint32_t*)(t + 2 F29_QTAB_N))[q]; 2.25 KiB
+// of the 3 KiB callers reserve); the caller's next __syncthreads publishes it.
+// Planes, not 48-byte entries: a wave's quotients q index the limb-8 words at
+// 4-byte stride, so lanes with distinct q < 32 hit distinct ds_read_b32 banks
+// (the 48-byte stride repeated banks every 8 values of q; tools/lds_banks.py)
 __device__ __forceinline__ void f29_qtab_init(uint4* t) {
     for (uint32_t q = threadIdx.x; q < F29_QTAB_N; q += blockDim.x) {
         uint32_t Q[9];
@@ -213,9 +217,15 @@ __device__ __forceinline__ void f29_qtab_init(uint4* t) {
 #pragma unroll
         for (int i = 1; i < 8; ++i) T[i] = (1u << 30) - 2u - Q[i];
         T[8] = 0u - 2u - Q[8];
+#ifdef LSP_QT_INTERLEAVED  // A/B switch (tools/variant_lib.py): round 5's 48-byte entries
         t[3 * q] = make_uint4(T[0], T[1], T[2], T[3]);
         t[3 * q + 1] = make_uint4(T[4], T[5], T[6], T[7]);
         t[3 * q + 2] = make_uint4(T[8], 0u, 0u, 0u);
+#else
+        t[q] = make_uint4(T[0], T[1], T[2], T[3]);
+        t[F29_QTAB_N + q] = make_uint4(T[4], T[5], T[6], T[7]);
+        reinterpret_cast<uint32_t*>(t + 2 * F29_QTAB_N)[q] = T[8];
+#endif
     }
 }
 
@@ -223,8 +233,13 @@ __device__ __forceinline__ F29 f29_reduce_qt(const F29& a, const uint4* __restri
     uint32_t q = __umulhi(a.l[8], 0xdb651d12u) >> 20;  // as f29_reduce
     // a value outside the documented bounds (top limb too large) would index past the table
     if (!LSP_BOUNDS(q < F29_QTAB_N)) q = 0;
+#ifdef LSP_QT_INTERLEAVED
     const uint4 x = t[3 * q], y = t[3 * q + 1];
     const uint32_t z = reinterpret_cast<const uint32_t*>(t + 3 * q + 2)[0];
+#else
+    const uint4 x = t[q], y = t[F29_QTAB_N + q];
+    const uint32_t z = reinterpret_cast<const uint32_t*>(t + 2 * F29_QTAB_N)[q];
+#endif
     const uint32_t T[9] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z};
     F29 o;
     uint32_t k = 0;

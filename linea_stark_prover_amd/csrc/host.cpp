@@ -394,21 +394,22 @@ lsp::HostPool& lsp_ctx::host_pool() {
 // counted are this process's affinity set (hardware_concurrency() counts the
 // whole machine: 256 on a box whose GPU share is 16).  When the launcher says
 // several ranks share this host (torchrun's LOCAL_WORLD_SIZE), the set is
-// divided among them only if it is the shared one -- the whole machine, or at
-// least 16 CPUs per rank; a smaller set is taken as this rank's own slice
-// (a launcher that pins each rank, e.g. --cpu-bind or numactl per rank), which
-// dividing again would shrink to a few threads.  LSP_HOST_THREADS overrides.
+// divided among them: the library cannot tell a set the ranks share from a
+// slice a launcher pinned for this rank alone, and of the two mistakes
+// dividing a private slice only makes the pool smaller, while not dividing a
+// shared one puts ranks x 16 spinning threads on it.  The Python
+// launch path (replicas.init_from_env) compares the ranks' sets and exports
+// the exact size as LSP_HOST_THREADS, which overrides this; other launchers
+// that pin each rank to its own CPUs set LSP_HOST_THREADS themselves (lsp.h).
 unsigned lsp::default_host_threads() {
     unsigned ranks = 1;
     if (const char* e = std::getenv("LOCAL_WORLD_SIZE")) ranks = (unsigned)std::max(1L, std::strtol(e, nullptr, 10));
-    const unsigned machine = std::max(1u, std::thread::hardware_concurrency());
-    unsigned cpus = machine;
+    unsigned cpus = std::max(1u, std::thread::hardware_concurrency());
 #if defined(__linux__)
     cpu_set_t set;
     if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) cpus = (unsigned)CPU_COUNT(&set);
 #endif
-    const bool shared = cpus >= machine || cpus >= ranks * 16u;
-    unsigned n = std::min(16u, std::max(1u, shared ? cpus / ranks : cpus));
+    unsigned n = std::min(16u, std::max(1u, cpus / ranks));
     if (const char* e = std::getenv("LSP_HOST_THREADS")) n = (unsigned)std::max(1L, std::strtol(e, nullptr, 10));
     return n;
 }

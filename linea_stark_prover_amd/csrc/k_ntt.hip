@@ -151,6 +151,49 @@ struct TileLds {
     }
 };
 
+// The LDS slot of tile element e: an XOR swizzle of its low bits by higher
+// bits, e ^ ((e >> 1) & 8) ^ ((e >> 2) & 31) (bits 2..6 -> 0..4, bit 4 -> 3).
+// Unswizzled, the radix-4 groups at distances 1 and 4 (and 2 and 8 with two
+// columns per row) put a wave's lanes on a quarter of the banks: 14 and 8.7
+// extra LDS cycles per instruction, 3.6 per LDS instruction over a pass, as
+// the PMC measured (SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS 3.9 / 3.1 / 2.2,
+// profiles/r05l_valu_pmc.txt).  This map makes every ds_read_b128 16-lane
+// group, ds_read/write_b32 32-lane half and ds_write_b128 8-lane group of
+// every radix-4 distance at 1 and 2 columns per row hit distinct banks (one
+// 2-way group left, the radix-2 stage at distance 1 with 2 columns), and at
+// 4 and 8 columns too (tools/lds_banks.py --swizzle ntt, found by the search
+// there; of the maps that do this, the cheapest found: two shift-mask terms,
+// half the VALU of the five-bit map tried first, which the fused pass paid
+// for: +5 % on a VALU-bound kernel).  It is XOR-linear and moves bits only downwards, so it permutes
+// [0, 2^j) for every j: the tile's size is unchanged, and a quad's members
+// e0 | m de (e0 zero at de's bits) sit at tswz(e0) ^ tswz(m de), one wave-
+// uniform XOR each.
+__device__ __forceinline__ uint32_t tswz(uint32_t e) {
+#ifdef LSP_NTT_NO_SWZ  // A/B switch (tools/variant_lib.py): the unswizzled tile
+    return e;
+#else
+    return e ^ ((e >> 1) & 8u) ^ ((e >> 2) & 31u);
+#endif
+}
+
+// The fused pass's twiddle cache in LDS, three planes as TileLds (limbs 0-3,
+// 4-7, 8): 36 bytes an entry instead of a 48-byte padded slot, and the limb-8
+// words at 4-byte stride (the 48-byte stride repeated ds_read_b32 banks every
+// 8 entries)
+struct TwlLds {
+    uint4* a;
+    uint4* b;
+    uint32_t* c;
+    __device__ __forceinline__ F29 get(uint32_t i) const {
+        const uint4 x = a[i], y = b[i];
+        F29 o;
+        o.l[0] = x.x; o.l[1] = x.y; o.l[2] = x.z; o.l[3] = x.w;
+        o.l[4] = y.x; o.l[5] = y.y; o.l[6] = y.z; o.l[7] = y.w;
+        o.l[8] = c[i];
+        return o;
+    }
+};
+
 // Two radix-2 stages in registers (radix-4 groups): per group 4 elements are
 // read from and written to the LDS once instead of twice, one barrier per two
 // stages, 3 twiddles per 4 butterflies, and the sums between the two stages
@@ -287,8 +330,8 @@ __device__ __forceinline__ uint32_t twl_index(const TileGeom<LOGCW>& gm, uint32_
 template <bool DIF, int LOGCW>
 __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOGCW>& gm, const uint4* __restrict__ tw,
                                             uint32_t s0, uint32_t logH, uint32_t n_el,
-                                            const uint4* twl = nullptr, const uint4* qt = nullptr,
-                                            uint32_t twl_n = 0) {
+                                            TwlLds twl = TwlLds{nullptr, nullptr, nullptr},
+                                            const uint4* qt = nullptr, uint32_t twl_n = 0) {
     constexpr uint32_t CW = 1u << LOGCW;
     const uint32_t k = gm.k, G = 1u << gm.logG;
     const uint32_t cshift = gm.logG + LOGCW;  // element index = (t << cshift) + (g << LOGCW) + c
@@ -298,9 +341,9 @@ __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOG
         // DIF w^((row mod H/2^(s+1)) 2^s), DIT w^((row mod 2^s) 2^(logH-1-s)); the
         // table is stage-major (entry 2^(m-1) - 1 + i = w_(2^m)^i), so
         // consecutive rows read consecutive slots
-        if (DIF && twl) {  // the fused pass's LDS copy
+        if (DIF && twl_n) {  // the fused pass's LDS copy
             const uint32_t ti = twl_index(gm, row, s);
-            return f29_load48(twl + 3 * (LSP_BOUNDS(ti < twl_n) ? ti : 0u));
+            return twl.get(LSP_BOUNDS(ti < twl_n) ? ti : 0u);
         }
         const uint32_t half = DIF ? (uint32_t)(H >> (s + 1)) : (1u << s);
         if (!LSP_BOUNDS(s < logH && row < H)) return f29_zero();
@@ -324,7 +367,10 @@ __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOG
                 const uint32_t t0 = ((pp & ~bmask) << 2) | (pp & bmask);
                 const uint32_t e0 = (t0 << cshift) + (g << LOGCW) + c, de = (1u << b) << cshift;
                 if (!LSP_BOUNDS(e0 + 3 * de < n_el && t0 + 3 * (1u << b) < k_pos(k))) continue;
-                F29 v0 = T.get(e0), v1 = T.get(e0 + de), v2 = T.get(e0 + 2 * de), v3 = T.get(e0 + 3 * de);
+                // e0 is zero at de's two bits: member m sits at tswz(e0) ^ tswz(m de)
+                const uint32_t x0 = tswz(e0), d1 = tswz(de), d2 = tswz(2 * de);
+                const uint32_t x1 = x0 ^ d1, x2 = x0 ^ d2, x3 = x1 ^ d2;
+                F29 v0 = T.get(x0), v1 = T.get(x1), v2 = T.get(x2), v3 = T.get(x3);
                 const uint32_t r0 = gm.row_of(t0, g), dr = (1u << b) << gm.logL;
                 if constexpr (DIF) {
                     if constexpr (TRIV)
@@ -337,10 +383,10 @@ __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOG
                     else
                         dit4<false>(v0, v1, v2, v3, tw_at(r0, s), tw_at(r0, s + 1), tw_at(r0 + dr, s + 1), qt);
                 }
-                T.put(e0, v0);
-                T.put(e0 + de, v1);
-                T.put(e0 + 2 * de, v2);
-                T.put(e0 + 3 * de, v3);
+                T.put(x0, v0);
+                T.put(x1, v1);
+                T.put(x2, v2);
+                T.put(x3, v3);
             }
         };
         if (DIF ? (s + 1 == logH - 1) : (s == 0))
@@ -359,8 +405,9 @@ __device__ __forceinline__ void tile_stages(const TileLds& T, const TileGeom<LOG
             const uint32_t pg = bf >> LOGCW;
             const uint32_t g = pg & (G - 1), pp = pg >> gm.logG;
             const uint32_t t0 = ((pp >> logd) << (logd + 1)) | (pp & dmask);
-            const uint32_t a0 = (t0 << cshift) + (g << LOGCW) + c, a1 = a0 + ((1u << logd) << cshift);
-            if (!LSP_BOUNDS(a1 < n_el)) continue;
+            const uint32_t e0 = (t0 << cshift) + (g << LOGCW) + c, e1 = e0 + ((1u << logd) << cshift);
+            if (!LSP_BOUNDS(e1 < n_el)) continue;
+            const uint32_t a0 = tswz(e0), a1 = a0 ^ tswz((1u << logd) << cshift);  // e0 zero at that bit
             const F29 a = T.get(a0), b = T.get(a1);
             if (trivial) {
                 T.put(a0, red(f29_lazy2(a, b), qt));
@@ -421,13 +468,16 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
 #endif
     constexpr uint32_t NREG = FWD_FIRST ? NTT_MAX_EL / NTT_THREADS : 1;
     F29 xr[NREG];
+    uint32_t xs[NREG];  // the fused pass: the LDS slots of this thread's elements, for every coset
     // the forward twiddles of this tile in LDS (after the tile and the per-row
     // twist factors; published by the barrier after the coefficient load below)
-    uint4* twl = nullptr;
+    // (by value: a pointer to it would put the struct in scratch memory)
+    TwlLds twl{nullptr, nullptr, nullptr};
     if (FWD_FIRST && p.twl_n) {
         const bool rt = !p.twist_per_col || p.ratio;  // the row factors sit between the tile and these
-        twl = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_raw) + (size_t)n_el * sizeof(F29) +
-                                       (rt ? (size_t)(K << logG) * sizeof(F29) : 0));
+        const size_t off = (size_t)n_el * sizeof(F29) + (rt ? (size_t)(K << logG) * sizeof(F29) : 0);
+        uint4* base = reinterpret_cast<uint4*>(reinterpret_cast<char*>(lds_raw) + ((off + 15) & ~(size_t)15));
+        twl = TwlLds{base, base + p.twl_n, reinterpret_cast<uint32_t*>(base + 2 * p.twl_n)};
         const uint32_t per = K - 1;  // entries per row group
         for (uint32_t e = threadIdx.x; e < p.twl_n; e += NTT_THREADS) {
             const uint32_t g = e / per, r = e - g * per;
@@ -438,9 +488,9 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
             const uint32_t half = (uint32_t)(H >> (sk + 1));
             const size_t gi = (size_t)(half - 1) + gm.gid0 + g + ((size_t)u << p.logL);
             if (!LSP_BOUNDS(gi + 1 < H && sk < p.k)) continue;
-            twl[3 * e] = p.tw[3 * gi];
-            twl[3 * e + 1] = p.tw[3 * gi + 1];
-            twl[3 * e + 2] = p.tw[3 * gi + 2];
+            twl.a[e] = p.tw[3 * gi];
+            twl.b[e] = p.tw[3 * gi + 1];
+            twl.c[e] = p.tw[3 * gi + 2].x;
         }
     }
     if (FWD_FIRST) {
@@ -451,14 +501,15 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
             uint32_t t, g, c;
             gm.split(e, t, g, c);
             if (c >= cw) {  // padding columns of the last chunk: zeros (the butterflies reduce them too)
-                T.put(gm.idx(t, g, c), f29_zero());
+                T.put(tswz(gm.idx(t, g, c)), f29_zero());
                 continue;
             }
             const uint32_t row = gm.row_of(t, g);
             const uint32_t srow = p.inv_gather ? brev_bits(row, p.logH) : row;
             size_t si;
             if (!LSP_BOUNDS(row < H && gm.idx(t, g, c) < n_el && c0 + c < p.w)) continue;
-            T.put(gm.idx(t, g, c), src_at(p.src_map, H, srow, c0 + c, si) ? f29_repack_in(p.src[si]) : f29_zero());
+            T.put(tswz(gm.idx(t, g, c)),
+                  src_at(p.src_map, H, srow, c0 + c, si) ? f29_repack_in(p.src[si]) : f29_zero());
         }
         __syncthreads();
         if (!p.no_inv) tile_stages<false, LOGCW>(T, gm, p.tw_inv, p.logH - p.k, p.logH, n_el);
@@ -467,7 +518,8 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
             const uint32_t e = threadIdx.x + j * NTT_THREADS;
             uint32_t t, g, c;
             gm.split(e, t, g, c);
-            if (e < n_el && c < cw) xr[j] = T.get(gm.idx(t, g, c));  // normalised, < 8.3 r
+            xs[j] = tswz(gm.idx(t, g, c));
+            if (e < n_el && c < cw) xr[j] = T.get(xs[j]);  // normalised, < 8.3 r
         }
     }
     F29* fac = reinterpret_cast<F29*>(T.c + n_el);  // K * G extra entries (launcher sizes the LDS for it)
@@ -504,7 +556,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
                 gm.split(e, t, g, c);
                 if (e >= n_el) continue;
                 if (c >= cw) {  // padding column: zero in the tile (never stored)
-                    T.put(gm.idx(t, g, c), f29_zero());
+                    T.put(xs[jr], f29_zero());
                     continue;
                 }
                 F29 f;
@@ -517,9 +569,9 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
                 }
                 if (chain) {
                     xr[jr] = f29_mul(xr[jr], f);  // < 8.2 r for inputs < 8.3 r and f < r, at every step
-                    T.put(gm.idx(t, g, c), xr[jr]);
+                    T.put(xs[jr], xr[jr]);
                 } else {
-                    T.put(gm.idx(t, g, c), f29_mul(xr[jr], f));  // < 8.3 r
+                    T.put(xs[jr], f29_mul(xr[jr], f));  // < 8.3 r
                 }
             }
         } else {
@@ -527,7 +579,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
                 uint32_t t, g, c;
                 gm.split(e, t, g, c);
                 if (c >= cw) {  // padding columns of the last chunk: zeros (the butterflies reduce them too)
-                    T.put(gm.idx(t, g, c), f29_zero());
+                    T.put(tswz(gm.idx(t, g, c)), f29_zero());
                     continue;
                 }
                 const uint32_t row = gm.row_of(t, g);
@@ -538,19 +590,31 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
                     v = src_at(p.src_map, H, brev_bits(row, p.logH), c0 + c, si) ? f29_repack_in(p.src[si]) : f29_zero();
                 else
                     v = f29_repack_in(base[(size_t)row * p.w + c0 + c]);
-                T.put(gm.idx(t, g, c), v);
+                T.put(tswz(gm.idx(t, g, c)), v);
             }
         }
         __syncthreads();
-        tile_stages<DIF, LOGCW>(T, gm, p.tw, p.s0, p.logH, n_el, twl, qt, p.twl_n);
+        tile_stages<DIF, LOGCW>(T, gm, p.tw, p.s0, p.logH, n_el, twl, qt, FWD_FIRST ? p.twl_n : 0u);
         // ---- store
         const bool canon = p.canon != 0;
-        for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
-            uint32_t t, g, c;
-            gm.split(e, t, g, c);
-            if (c >= cw) continue;
-            if (!LSP_BOUNDS(gm.row_of(t, g) < H && gm.idx(t, g, c) < n_el && c0 + c < p.w)) continue;
-            base[(size_t)gm.row_of(t, g) * p.w + c0 + c] = f29_store(T.get(gm.idx(t, g, c)), canon);
+        if constexpr (FWD_FIRST) {  // this thread's elements, at the slots computed once (xs)
+#pragma unroll
+            for (uint32_t jr = 0; jr < NREG; ++jr) {
+                const uint32_t e = threadIdx.x + jr * NTT_THREADS;
+                uint32_t t, g, c;
+                gm.split(e, t, g, c);
+                if (e >= n_el || c >= cw) continue;
+                if (!LSP_BOUNDS(gm.row_of(t, g) < H && gm.idx(t, g, c) < n_el && c0 + c < p.w)) continue;
+                base[(size_t)gm.row_of(t, g) * p.w + c0 + c] = f29_store(T.get(xs[jr]), canon);
+            }
+        } else {
+            for (uint32_t e = threadIdx.x; e < n_el; e += NTT_THREADS) {
+                uint32_t t, g, c;
+                gm.split(e, t, g, c);
+                if (c >= cw) continue;
+                if (!LSP_BOUNDS(gm.row_of(t, g) < H && gm.idx(t, g, c) < n_el && c0 + c < p.w)) continue;
+                base[(size_t)gm.row_of(t, g) * p.w + c0 + c] = f29_store(T.get(tswz(gm.idx(t, g, c))), canon);
+            }
         }
     }
 }
@@ -731,10 +795,10 @@ static hipError_t run_lde(LdeWhat what, const Fr* in, ColMap map, Fr* X, Fr* out
         // tile, plus one twist (or chain ratio) factor per row in the fused pass
         const bool fac = mode == PASS_INV_FWD && (!twist_per_col || ratio);
         size_t lds = ((size_t(1) << (k + logG)) * CW + (fac ? (size_t(1) << (k + logG)) : 0)) * sizeof(F29);
-        // ... and its forward twiddles when they fit (<= 512 entries, 24 KiB: 2 workgroups per CU)
+        // ... and its forward twiddles when they fit (<= 512 entries, 18 KiB in planes: 2 workgroups per CU)
         const size_t twl_n = (size_t(1) << logG) * ((size_t(1) << k) - 1);
         p.twl_n = (mode == PASS_INV_FWD && twl_n <= 512 && twl_env) ? (uint32_t)twl_n : 0u;
-        lds += (size_t)p.twl_n * 3 * sizeof(uint4);
+        if (p.twl_n) lds = ((lds + 15) & ~(size_t)15) + (size_t)p.twl_n * (2 * sizeof(uint4) + sizeof(uint32_t));
         if (mode != PASS_INV_FWD) lds += (size_t)F29_QTAB_N * 3 * sizeof(uint4);  // k_ntt_rm's reduction table
         p.xcd = (tiles / nchunk) % 8 == 0 ? 1u : 0u;
         const dim3 grid((unsigned)tiles), blk(256);

@@ -357,65 +357,152 @@ ExchangePlan exchange_plan(const Comm& comm, size_t h, size_t w, size_t q, uint3
     return p;
 }
 
+// median wall ms of `reps` runs of f after one warm-up, `before` ahead of each
+// run outside the timing (the calibration's barrier)
+static double median_ms(lsp_ctx* ctx, const std::function<void()>& f, int reps, const std::function<void()>& before) {
+    std::vector<double> t;
+    for (int r = 0; r <= reps; ++r) {
+        if (before) before();
+        LSP_HIP(hipStreamSynchronize(ctx->stream));
+        const auto t0 = std::chrono::steady_clock::now();
+        f();
+        LSP_HIP(hipStreamSynchronize(ctx->stream));
+        if (r) t.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+
+// This GPU's inverse-NTT rate (G elements/s) over an h x w matrix of seeded
+// random field elements, h = 2^log_h.  Random operands, not zeros: the chip
+// is power-held on MAD-dense work (2.1 against 2.4 GHz), and zero limbs draw
+// less power, so an all-zero probe overstates the rate.
+// Buffers "calib_intt_x/y" (calibrate_exchange allocates them before its first
+// collective; the caller releases them).
+double calibrate_intt(lsp_ctx* ctx, uint32_t log_h, size_t w, int reps, const std::function<void()>& before) {
+    const size_t h = (size_t)1 << log_h;
+    Fr* x = ctx->fbuf("calib_intt_x", h * w);
+    Fr* y = ctx->fbuf("calib_intt_y", h * w);
+    // h x w values (the raw-column generator: column-major, read here as rows)
+    LSP_HIP(launch_gen_raw_perm(0x43414c4942ull /* "CALIB" */, h, (uint32_t)w, 1, 0, x, y, ctx->stream));
+    const uint4* tw = ctx->twiddle29(log_h, true);
+    // device time between events around a burst of 8 back-to-back inverses
+    // (what a proof's phase timer sees of a GPU that is busy): host wall time
+    // adds launch and synchronisation latency, and one inverse after an idle
+    // gap runs at a clock still ramping up -- 10-13 % slower than the proofs'
+    // own phase at 2^20 x 4 (tests/test_gpu_calibration.py)
+    constexpr int burst = 8;
+    auto inv = [&] { LSP_HIP(launch_intt(x, ColMap::plain((uint32_t)w), y, w, log_h, tw, ctx->stream)); };
+    hipEvent_t e0, e1;
+    LSP_HIP(hipEventCreate(&e0));
+    LSP_HIP(hipEventCreate(&e1));
+    std::vector<double> t;
+    for (int r = 0; r <= reps; ++r) {
+        if (before) before();
+        if (!r)
+            for (int i = 0; i < burst; ++i) inv();  // warm-up burst
+        LSP_HIP(hipEventRecord(e0, ctx->stream));
+        for (int i = 0; i < burst; ++i) inv();
+        LSP_HIP(hipEventRecord(e1, ctx->stream));
+        LSP_HIP(hipEventSynchronize(e1));
+        float ms = 0;
+        LSP_HIP(hipEventElapsedTime(&ms, e0, e1));
+        if (r) t.push_back(ms / burst);
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    std::sort(t.begin(), t.end());
+    return (double)(h * w) / (t[t.size() / 2] * 1e-3) / 1e9;
+}
+
 void calibrate_exchange(lsp_ctx* ctx, Comm& comm) {
     if (comm.size < 2 || comm.rehearsal()) return;
     hipStream_t st = ctx->stream;
     const size_t G = (size_t)comm.size;
-    auto timed = [&](const std::function<void()>& f, int reps) {  // median wall ms of reps runs after a warm-up
-        std::vector<double> t;
-        for (int r = 0; r <= reps; ++r) {
-            LSP_HIP(hipStreamSynchronize(st));
-            const auto t0 = std::chrono::steady_clock::now();
-            f();
-            LSP_HIP(hipStreamSynchronize(st));
-            if (r) t.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-        }
-        std::sort(t.begin(), t.end());
-        return t[t.size() / 2];
-    };
-    // the minimum of each value over the ranks: every rank then takes the same
-    // branch below and plans the same exchange (a rank-dependent branch would
-    // issue a collective some ranks skip -- RCCL hangs on that)
-    auto agree_min = [&](std::vector<double> mine) {
+    comm.ag_gbs = comm.intt_gelem_s = 0;
+    comm.calib_raw.clear();
+    // every rank's k values, in rank order (one small allgather)
+    double* ds = (double*)ctx->buf("calib_ds", 4 * sizeof(double));
+    double* dr = (double*)ctx->buf("calib_dr", 4 * sizeof(double) * G);
+    auto gather = [&](const std::vector<double>& mine) {
         const size_t k = mine.size();
-        double* ds = (double*)ctx->buf("calib_ds", k * sizeof(double));
-        double* dr = (double*)ctx->buf("calib_dr", k * sizeof(double) * G);
         LSP_HIP(hipMemcpyAsync(ds, mine.data(), k * sizeof(double), hipMemcpyHostToDevice, st));
         comm.allgather(ctx, ds, dr, k * sizeof(double), "calibration");
         std::vector<double> all(k * G);
         LSP_HIP(hipMemcpyAsync(all.data(), dr, all.size() * sizeof(double), hipMemcpyDeviceToHost, st));
         LSP_HIP(hipStreamSynchronize(st));
-        for (size_t r = 1; r < G; ++r)
-            for (size_t i = 0; i < k; ++i) mine[i] = std::min(mine[i], all[r * k + i]);
-        for (size_t i = 0; i < k; ++i) mine[i] = std::min(mine[i], all[i]);
-        return mine;
+        return all;
     };
+    // a barrier ahead of every timed rep, so no rank's time includes waiting for a late peer
+    auto barrier = [&] {
+        LSP_HIP(hipMemsetAsync(ds, 0, sizeof(double), st));
+        comm.allgather(ctx, ds, dr, sizeof(double), "calibration barrier");
+        LSP_HIP(hipStreamSynchronize(st));
+    };
+    // Every buffer first: a rank that cannot allocate must not
+    // leave its peers blocked in a collective it never joins.  The ranks agree
+    // on success with one allgather; on any failure all of them skip the
+    // probes and stay uncalibrated (the split exchange), consistently.
+    const uint32_t logh = 20;
+    const size_t h = (size_t)1 << logh, w = 8;
+    const size_t big = (size_t)256 << 20, share_big = std::max<size_t>(big / G / 256, 1) * 256;
+    double ok = 1;
+    try {
+        ctx->buf("calib_s", share_big);
+        ctx->buf("calib_r", share_big * G);
+        ctx->fbuf("calib_intt_x", h * w);
+        ctx->fbuf("calib_intt_y", h * w);
+        ctx->twiddle29(logh, true);
+    } catch (const LspError&) {
+        ok = 0;
+        (void)hipGetLastError();
+    }
+    const std::vector<double> oks = gather({ok});
+    if (*std::min_element(oks.begin(), oks.end()) == 0) {
+        comm.calib_status = "skipped: a rank could not allocate the probe buffers";
+        ctx->release("calib_");
+        return;
+    }
     // the allgather: a 4 MiB probe first; only a transport that is not clearly
     // below the break-even region (>= 20 GB/s on every rank) gets the 256 MiB one
     auto probe = [&](size_t total) {
         const size_t share = std::max<size_t>(total / G / 256, 1) * 256;
-        char* s = (char*)ctx->buf("calib_s", share);
-        char* r = (char*)ctx->buf("calib_r", share * G);
+        char* s = (char*)ctx->buf("calib_s", share_big);
+        char* r = (char*)ctx->buf("calib_r", share_big * G);
         LSP_HIP(hipMemsetAsync(s, comm.rank & 0xff, share, st));
-        const double ms = timed([&] { comm.allgather(ctx, s, r, share, "calibration"); }, 3);
+        const double ms = median_ms(ctx, [&] { comm.allgather(ctx, s, r, share, "calibration"); }, 3, barrier);
         comm.ag_probe_bytes = share * G;
         return (double)((G - 1) * share) / (ms * 1e-3) / 1e9;
     };
-    double gbs = agree_min({probe((size_t)4 << 20)})[0];
-    if (gbs >= 20) gbs = probe((size_t)256 << 20);
-    // the inverse NTT the split distributes: 8 columns of 2^20 (3 passes like the proofs' sizes)
-    const uint32_t logh = 20;
-    const size_t h = (size_t)1 << logh, w = 8;
-    Fr* x = ctx->fbuf("calib_x", h * w);
-    Fr* y = ctx->fbuf("calib_y", h * w);
-    LSP_HIP(hipMemsetAsync(x, 0, h * w * sizeof(Fr), st));
-    const uint4* tw = ctx->twiddle29(logh, true);
-    const double ms =
-        timed([&] { LSP_HIP(launch_intt(x, ColMap::plain((uint32_t)w), y, w, logh, tw, st)); }, 3);
-    const std::vector<double> agreed = agree_min({gbs, (double)(h * w) / (ms * 1e-3) / 1e9});
-    comm.ag_gbs = agreed[0];
-    comm.intt_gelem_s = agreed[1];
+    const double small = probe((size_t)4 << 20);
+    const std::vector<double> smalls = gather({small});
+    const bool go_big = *std::min_element(smalls.begin(), smalls.end()) >= 20;  // the same on every rank
+    const double large = go_big ? probe(big) : 0.0;
+    if (!go_big) comm.ag_probe_bytes = std::max<size_t>(((size_t)4 << 20) / G / 256, 1) * 256 * G;
+    // the inverse NTT the split distributes: 8 columns of 2^20 of random field elements
+    const double intt = calibrate_intt(ctx, logh, w, 3, barrier);
+    comm.calib_raw = gather({small, large, intt});  // 3 per rank, rank order (lsp_comm_calibration)
+    double gbs = 1e300, rate = 1e300;
+    for (size_t r = 0; r < G; ++r) {
+        gbs = std::min(gbs, go_big ? comm.calib_raw[3 * r + 1] : comm.calib_raw[3 * r]);
+        rate = std::min(rate, comm.calib_raw[3 * r + 2]);
+    }
+    comm.ag_gbs = gbs;
+    comm.intt_gelem_s = rate;
+    comm.calib_status = go_big ? "calibrated (4 MiB and 256 MiB allgather probes, random-data inverse NTT)"
+                               : "calibrated (4 MiB allgather probe below 20 GB/s, random-data inverse NTT)";
     ctx->release("calib_");
+}
+
+QuotientExchange quotient_exchange(const Comm& comm, size_t h, size_t q, uint32_t log_blowup) {
+    QuotientExchange x{0, 0, 0};
+    const size_t G = (size_t)comm.size;
+    if (G < 2 || q == 0) return x;
+    const size_t N = h << log_blowup, S = N / G, Q = q * h, Sq = std::min(S, Q);
+    x.bcasts = Q / Sq;
+    x.bytes_each = Sq * sizeof(Fr);
+    if (comm.ag_gbs > 0) x.model_ms = (double)(x.bcasts * x.bytes_each) / (comm.ag_gbs * 1e9) * 1e3;
+    return x;
 }
 
 // ------------------------------------------------------------- Merkle
@@ -925,7 +1012,9 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
             ColMap m = ColMap::plain((uint32_t)w);
             m.c0 = (uint32_t)host_bitrev(g, b);
             m.cstep = G;
+            T.begin("trace inverse NTT");  // this rank's cg columns (tests/test_gpu_calibration.py)
             LSP_HIP(launch_intt(d_trace, m, xl, cg, log_h, ctx->twiddle29(log_h, true), st));
+            T.end("trace inverse NTT");
             comm.allgather(ctx, xl, coef, h * cg * sizeof(Fr), "trace coefficients");
             tcoef = coef;
             tmap = ColMap::blocked(b, cg);

@@ -1,4 +1,5 @@
 #pragma once
+#include <functional>
 #include <vector>
 
 #include "host.hpp"
@@ -33,8 +34,20 @@ lsp_proof* prove_shard(lsp_ctx* ctx, Comm& comm, const Fr* d_trace, size_t h, si
                        const Fr* pub, size_t npub);
 // collective (every rank of comm): time an allgather of up to 256 MiB and this
 // GPU's inverse NTT, agree on the minimum over the ranks (comm.ag_gbs,
-// comm.intt_gelem_s)
+// comm.intt_gelem_s; every rank's raw values in comm.calib_raw)
 void calibrate_exchange(lsp_ctx* ctx, Comm& comm);
+// this GPU's inverse-NTT rate (G elements/s) on an h x w matrix of seeded
+// random elements, h = 2^log_h: median of `reps` after a warm-up, `before`
+// ahead of each rep (may be empty)
+double calibrate_intt(lsp_ctx* ctx, uint32_t log_h, size_t w, int reps, const std::function<void()>& before);
+// the quotient-chunk broadcasts a sharded proof of h rows with q chunks issues
+// on comm (either exchange choice): their count, bytes each, and their time
+// at the calibrated allgather bandwidth (0 when uncalibrated)
+struct QuotientExchange {
+    size_t bcasts, bytes_each;
+    double model_ms;
+};
+QuotientExchange quotient_exchange(const Comm& comm, size_t h, size_t q, uint32_t log_blowup);
 // the inverse-NTT exchange a sharded proof of h x w (q quotient chunks) over
 // comm makes: true = split by columns + an allgather of the coefficients,
 // false = every rank inverts every column (LSP_SHARD_SPLIT_INTT=0/1 forces

@@ -343,9 +343,37 @@ class Context:
         self._chk(L.lib().lsp_comm_exchange_plan(self.h, h, w, q, ctypes.byref(gbs), ctypes.byref(rate),
                                                  ctypes.byref(probe), ctypes.byref(split), ctypes.byref(ms_ag),
                                                  ctypes.byref(ms_red)))
-        return {"allgather_gbs": gbs.value, "intt_gelem_per_s": rate.value, "probe_bytes": probe.value,
-                "split_intt": bool(split.value), "model_allgather_ms": ms_ag.value,
-                "model_redundant_intt_ms": ms_red.value}
+        out = {"allgather_gbs": gbs.value, "intt_gelem_per_s": rate.value, "probe_bytes": probe.value,
+               "split_intt": bool(split.value), "model_allgather_ms": ms_ag.value,
+               "model_redundant_intt_ms": ms_red.value, "per_rank": self.comm_calibration()}
+        if q:
+            # the quotient-chunk broadcasts (the same bytes under either choice)
+            nb, each, qms = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_double()
+            self._chk(L.lib().lsp_comm_quotient_exchange(self.h, h, q, ctypes.byref(nb), ctypes.byref(each),
+                                                         ctypes.byref(qms)))
+            out.update({"quotient_bcasts": nb.value, "quotient_bcast_bytes_each": each.value,
+                        "model_quotient_bcast_ms": qms.value,
+                        "model_exchange_ms": qms.value + (ms_ag.value if split.value else 0.0)})
+        return out
+
+    def comm_calibration(self) -> list:
+        """lsp_comm_calibration: every rank's own probes, rank order --
+        {"allgather_4mib_gbs", "allgather_256mib_gbs" (0: not run), "intt_gelem_per_s"}"""
+        n = ctypes.c_size_t()
+        self._chk(L.lib().lsp_comm_calibration(self.h, None, 0, ctypes.byref(n)))
+        if not n.value:
+            return []
+        buf = (ctypes.c_double * n.value)()
+        self._chk(L.lib().lsp_comm_calibration(self.h, buf, n.value, ctypes.byref(n)))
+        v = list(buf)
+        return [{"allgather_4mib_gbs": v[i], "allgather_256mib_gbs": v[i + 1], "intt_gelem_per_s": v[i + 2]}
+                for i in range(0, len(v), 3)]
+
+    def calibrate_intt(self, log_h: int = 20, w: int = 8) -> float:
+        """lsp_calibrate_intt: this GPU's inverse-NTT rate on random data, G elements/s"""
+        v = ctypes.c_double()
+        self._chk(L.lib().lsp_calibrate_intt(self.h, log_h, w, ctypes.byref(v)))
+        return v.value
 
     def host_threads(self) -> int:
         """lsp_ctx_host_threads: the size of this context's host pool"""

@@ -134,6 +134,9 @@ class RawTrace:
 
     def push_traces(self, permutation_traces: Sequence[RawPermutationTrace],
                     lookup_traces: Sequence[RawLookupTrace]) -> List:
+        for lt in lookup_traces:  # one filter per table: the scratch below holds that many
+            if len(lt.b_filter) > len(lt.b):
+                raise ValueError(f"RawLookupTrace has {len(lt.b_filter)} b_filter columns for {len(lt.b)} tables")
         h = 0
         for t in list(lookup_traces) + list(permutation_traces):
             h = max(h, t.get_max_height())
@@ -146,7 +149,8 @@ class RawTrace:
         # largest block's), instead of an allocation and a synchronizing free per block
         raw = [len(t.a) + sum(len(x) for x in t.b) + 1 + len(t.b) for t in lookup_traces] + \
               [len(t.a) + len(t.b) for t in permutation_traces]
-        self._scratch = self.ctx.dev_alloc(max(max(raw, default=1) * h * 32, 32))
+        self._scratch_bytes = max(max(raw, default=1) * h * 32, 32)
+        self._scratch = self.ctx.dev_alloc(self._scratch_bytes)
         try:
             cfgs, col = [], 0
             for lt in lookup_traces:  # lookups first (trace/src/lib.rs:81-89)
@@ -169,7 +173,7 @@ class RawTrace:
         na, nb = len(pt.a), len(pt.b)
         da = self._scratch
         db = self._upload_cols(pt.a, n, da)
-        self._upload_cols(pt.b, n, db)
+        assert self._upload_cols(pt.b, n, db) - da <= self._scratch_bytes, "raw columns overran the scratch buffer"
         self.ctx._chk(L.lib().lsp_witness_permutation(
             self.ctx.h, da, na, db, nb, n, _ptr(self.alpha), _ptr(self.delta), self.ptr, self.width, col0,
             L.LSP_MEM_DEVICE))
@@ -184,6 +188,8 @@ class RawTrace:
         ptrs = [self._scratch]
         for cols in (lt.a, [c for t in lt.b for c in t], [lt.a_filter], list(lt.b_filter)):
             ptrs.append(self._upload_cols(cols, n, ptrs[-1]))
+        # the scratch was sized in push_traces for exactly these columns
+        assert ptrs[-1] - self._scratch <= self._scratch_bytes, "raw columns overran the scratch buffer"
         self.ctx._chk(L.lib().lsp_witness_lookup(
             self.ctx.h, ptrs[0], na, ptrs[1], nt, nbc, ptrs[2], ptrs[3], n, _ptr(self.alpha),
             _ptr(self.delta), self.ptr, self.width, col0, L.LSP_MEM_DEVICE))

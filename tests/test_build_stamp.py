@@ -93,11 +93,27 @@ def test_backdated_source_edit_rebuilds_not_relabels(tree):
     assert B.library_hash() == B.source_hash()
 
 
-def test_missing_stamp_forces_rebuild(tree):
+def test_missing_library_stamp_relinks(tree):
+    """objects whose own stamps match their sources are kept; the library is
+    relinked from them and stamped"""
     root, csrc, log = tree
     B.build(verbose=False)
     n = len(_log(log))
     os.remove(B.LIB + ".src")
+    B.build(verbose=False)
+    again = _log(log)[n:]
+    assert [l.split()[0] for l in again] == ["link"]
+    assert B.library_hash() == B.source_hash()
+
+
+def test_header_edit_recompiles_everything(tree):
+    root, csrc, log = tree
+    B.build(verbose=False)
+    n = len(_log(log))
+    hdr = root / "include" / "lsp.h"
+    t = os.path.getmtime(hdr)
+    hdr.write_text("/* header, edited */\n")
+    os.utime(hdr, (t - 100, t - 100))  # older than every object
     B.build(verbose=False)
     again = _log(log)[n:]
     assert sum(l.startswith("compile") for l in again) == 2 and again[-1].startswith("link")

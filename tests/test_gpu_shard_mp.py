@@ -40,6 +40,15 @@ def _run(tmp_path, nproc, comm, port, log_n=10, schedules=None, env_extra=None, 
         assert ex["allgather_gbs"] > 0 and ex["intt_gelem_per_s"] > 0 and ex["probe_bytes"] > 0, ex
         assert isinstance(ex["split_intt"], bool)
         assert ("trace coefficients" in {x["tag"] for x in rows}) == ex["split_intt"]
+        # every rank's raw probes (the minimum of which the plan used), and the
+        # quotient-chunk broadcasts the model prices beside the trace exchange
+        assert len(ex["per_rank"]) == nproc and all(r["intt_gelem_per_s"] > 0 and r["allgather_4mib_gbs"] > 0
+                                                      for r in ex["per_rank"]), ex
+        assert min(r["intt_gelem_per_s"] for r in ex["per_rank"]) == pytest.approx(ex["intt_gelem_per_s"])
+        qrows = [x for x in rows if x["tag"] in ("quotient chunk coefficients", "quotient values")]
+        assert len(qrows) == ex["quotient_bcasts"] and all(x["bytes"] == ex["quotient_bcast_bytes_each"]
+                                                            for x in qrows), (qrows, ex)
+        assert ex["model_quotient_bcast_ms"] > 0
         if plans is not None:
             plans.append(ex)
     if schedules is not None and comm == "gloo":

@@ -148,22 +148,21 @@ print(Context(StarkConfig(), device=-1).host_threads())
 """
 
 
-def _shared(aff, ranks):  # host.cpp default_host_threads: the set is the shared one
-    return aff >= (os.cpu_count() or 1) or aff >= 16 * ranks
-
-
 @pytest.mark.parametrize("env,cpus,expect", [
     ({"LSP_HOST_THREADS": "3"}, 0, lambda n: 3),
     ({"LOCAL_WORLD_SIZE": "1"}, 0, lambda n: min(16, n)),
-    # the process's whole set (here the machine's) is shared by the local ranks: divided
-    ({"LOCAL_WORLD_SIZE": "4"}, 0, lambda n: max(1, min(16, n // 4 if _shared(n, 4) else n))),
-    # a 2-CPU slice smaller than the machine (and < 16 per rank) is this rank's own: not divided again
-    ({"LOCAL_WORLD_SIZE": "8"}, 2, lambda n: 2),
+    # the process's set is divided among the local ranks
+    ({"LOCAL_WORLD_SIZE": "4"}, 0, lambda n: max(1, min(16, n // 4))),
+    # a small set several ranks may share (8 ranks on a 2-CPU cpuset) is divided too:
+    # never ranks x pool threads on a few CPUs; a launcher that pinned this slice for one rank
+    # says so with LSP_HOST_THREADS (replicas.init_from_env does)
+    ({"LOCAL_WORLD_SIZE": "8"}, 2, lambda n: 1),
+    ({"LOCAL_WORLD_SIZE": "8", "LSP_HOST_THREADS": "2"}, 2, lambda n: 2),
 ])
 def test_host_pool_size(product_lib, env, cpus, expect):
-    """the host pool divides the CPU set among LOCAL_WORLD_SIZE ranks
-    only when the set is the shared one (the machine's, or >= 16 CPUs per rank);
-    a launcher that pins each rank to its own slice keeps that slice"""
+    """the host pool divides the process's CPU set among the
+    LOCAL_WORLD_SIZE ranks (the library cannot tell a shared set from a pinned
+    slice, and dividing is the safe mistake); LSP_HOST_THREADS overrides"""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

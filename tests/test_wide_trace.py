@@ -39,3 +39,18 @@ def test_wide_proof_python_vs_c(oracle_lib):
     cb = oracle_lib.prove(p, oracle_lib.fr_buf([x for r in rows for x in r]), 8, len(rows[0]),
                           oracle_lib.air_desc(cfgs))
     assert cb == O.serialize_proof(pf)
+
+
+def test_push_traces_rejects_extra_b_filters(product_lib):
+    """more b_filter columns than tables would overrun the raw-column
+    scratch on the device; push_traces refuses them before allocating anything"""
+    import numpy as np
+    import pytest
+    from linea_stark_prover_amd.prover import Context, StarkConfig
+    from linea_stark_prover_amd.trace import RawLookupTrace, RawTrace
+    one = np.ones((4, 4), np.uint64)
+    lt = RawLookupTrace([one], [[one]], None, [one, one])  # 1 table, 2 filters
+    with Context(StarkConfig(), device=-1) as ctx:
+        rt = RawTrace(ctx, [np.zeros(4, np.uint64), np.zeros(4, np.uint64)])
+        with pytest.raises(ValueError, match="b_filter"):
+            rt.push_traces([], [lt])

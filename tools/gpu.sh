@@ -19,6 +19,10 @@
 #   py:<script>      python <script> under a 300 s limit (tools/ implied), output to a log
 #   h2d              tools/ubench/h2d: host -> device upload modes for a 128 MiB trace (build it first)
 #   tests900:<files> the listed test files with a 900 s per-test limit (the full-size oracle comparisons)
+#   pmclds:<lib>     one rocprofv3 --pmc pass of the LDS counters (SQ_INSTS_LDS SQ_WAIT_INST_LDS
+#                    SQ_LDS_BANK_CONFLICT) over a 2^19 prove on the library _ab/<lib>.so
+#   ktrace:<lib>     rocprofv3 kernel trace (+ --stats) of 2^19 proves on _ab/<lib>.so, summarised
+#                    per kernel (tools/prof_summary.py)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -88,6 +92,18 @@ for l in open('$log'):
       timeout -k 10 1100 python -u -m pytest -x -v --timeout 900 --timeout-method thread $files >> $log 2>&1 \
         || fail "$step" $log
       grep -E "passed|failed" $log | tail -1 ;;
+    pmclds:*)
+      lib=${step#pmclds:}
+      d=gpurun_out/pmclds_${lib}_$TAG
+      LSP_LIB=$PWD/_ab/$lib.so LSP_LIB_OLDER=1 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT \
+        --output-format csv -d $d -o run -- python3 tools/time_prove.py 19 > $d.log 2>&1 || fail "$step" $d.log
+      python tools/pmc_lds_summary.py $d/run_counter_collection.csv | tee $d.txt ;;
+    ktrace:*)
+      lib=${step#ktrace:}
+      d=gpurun_out/ktrace_${lib}_$TAG
+      LSP_LIB=$PWD/_ab/$lib.so LSP_LIB_OLDER=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d $d -o run -- python3 tools/time_prove.py 19 > $d.log 2>&1 || fail "$step" $d.log
+      python tools/prof_summary.py $d/run_kernel_stats.csv 4 > $d.txt 2>&1; head -25 $d.txt ;;
     py:*)
       script=${step#py:}
       log=gpurun_out/$(basename ${script%% *} .py)_$TAG.log

@@ -168,22 +168,43 @@ struct TileLds {
 // [0, 2^j) for every j: the tile's size is unchanged, and a quad's members
 // e0 | m de (e0 zero at de's bits) sit at tswz(e0) ^ tswz(m de), one wave-
 // uniform XOR each.
+//
+// Measured (round 6, profiles/r06_lds_swizzle.txt): the swizzle takes the
+// passes' SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS from 3.9 / 2.2 / 3.1 to 0.2 / 0.4
+// / 0.2 and their LDS wait share from 6.6 / 2.8 / 3.6 to 3.4 / 1.4 / 2.1 per
+// LDS instruction -- and the LDE's time not at all (2^19 x 8: 3.183 against
+// 3.179 ms, medians of 8 alternating runs), while whole proofs ran 0.22-0.27
+// ms slower with it (paired, both orders): the passes are VALU-bound, the
+// conflicts were hidden behind the other waves' VALU work, and the map's
+// instructions are not.  So the tile ships unswizzled; LSP_NTT_SWZ builds it
+// (tools/variant_lib.py).
 __device__ __forceinline__ uint32_t tswz(uint32_t e) {
-#ifdef LSP_NTT_NO_SWZ  // A/B switch (tools/variant_lib.py): the unswizzled tile
-    return e;
-#else
+#ifdef LSP_NTT_SWZ
     return e ^ ((e >> 1) & 8u) ^ ((e >> 2) & 31u);
+#else
+    return e;
 #endif
 }
 
-// The fused pass's twiddle cache in LDS, three planes as TileLds (limbs 0-3,
-// 4-7, 8): 36 bytes an entry instead of a 48-byte padded slot, and the limb-8
-// words at 4-byte stride (the 48-byte stride repeated ds_read_b32 banks every
-// 8 entries)
+// The fused pass's twiddle cache in LDS: 48-byte slots (limbs 0-3, 4-7, 8 +
+// padding), read by f29_load48.  LSP_NTT_TWL_PLANES stores it in three planes
+// as TileLds instead (36 bytes an entry, the limb-8 words at 4-byte stride, so
+// distinct entries never share a ds_read_b32 bank within 32 of them): measured
+// 2 % slower over the whole LDE (2^19 x 8: 3.207 against 3.131 ms,
+// profiles/r06_lds_swizzle.txt), so the slots stay.
 struct TwlLds {
     uint4* a;
     uint4* b;
     uint32_t* c;
+#ifndef LSP_NTT_TWL_PLANES  // 48-byte slots, all in `a` (the planes are the A/B variant)
+    __device__ __forceinline__ F29 get(uint32_t i) const { return f29_load48(a + 3 * i); }
+    __device__ __forceinline__ void put(uint32_t i, const uint4* src) const {
+        a[3 * i] = src[0];
+        a[3 * i + 1] = src[1];
+        a[3 * i + 2] = src[2];
+    }
+    static constexpr size_t BYTES = 3 * sizeof(uint4);
+#else
     __device__ __forceinline__ F29 get(uint32_t i) const {
         const uint4 x = a[i], y = b[i];
         F29 o;
@@ -192,6 +213,13 @@ struct TwlLds {
         o.l[8] = c[i];
         return o;
     }
+    __device__ __forceinline__ void put(uint32_t i, const uint4* src) const {
+        a[i] = src[0];
+        b[i] = src[1];
+        c[i] = src[2].x;
+    }
+    static constexpr size_t BYTES = 2 * sizeof(uint4) + sizeof(uint32_t);
+#endif
 };
 
 // Two radix-2 stages in registers (radix-4 groups): per group 4 elements are
@@ -488,9 +516,7 @@ __global__ __launch_bounds__(NTT_THREADS) void k_ntt_rm(NttPass p) {
             const uint32_t half = (uint32_t)(H >> (sk + 1));
             const size_t gi = (size_t)(half - 1) + gm.gid0 + g + ((size_t)u << p.logL);
             if (!LSP_BOUNDS(gi + 1 < H && sk < p.k)) continue;
-            twl.a[e] = p.tw[3 * gi];
-            twl.b[e] = p.tw[3 * gi + 1];
-            twl.c[e] = p.tw[3 * gi + 2].x;
+            twl.put(e, p.tw + 3 * gi);
         }
     }
     if (FWD_FIRST) {
@@ -798,7 +824,7 @@ static hipError_t run_lde(LdeWhat what, const Fr* in, ColMap map, Fr* X, Fr* out
         // ... and its forward twiddles when they fit (<= 512 entries, 18 KiB in planes: 2 workgroups per CU)
         const size_t twl_n = (size_t(1) << logG) * ((size_t(1) << k) - 1);
         p.twl_n = (mode == PASS_INV_FWD && twl_n <= 512 && twl_env) ? (uint32_t)twl_n : 0u;
-        if (p.twl_n) lds = ((lds + 15) & ~(size_t)15) + (size_t)p.twl_n * (2 * sizeof(uint4) + sizeof(uint32_t));
+        if (p.twl_n) lds = ((lds + 15) & ~(size_t)15) + (size_t)p.twl_n * TwlLds::BYTES;
         if (mode != PASS_INV_FWD) lds += (size_t)F29_QTAB_N * 3 * sizeof(uint4);  // k_ntt_rm's reduction table
         p.xcd = (tiles / nchunk) % 8 == 0 ? 1u : 0u;
         const dim3 grid((unsigned)tiles), blk(256);

@@ -120,6 +120,14 @@ def test_configs2_wide_2e20_oracle_checks(gpu_ctx, oracle_lib):
     proof = gpu_ctx.prove(trace, air, pub)
     assert gpu_ctx.verify(proof, air, pub)
     assert oracle_lib.verify(p, proof, list(air.descriptor())) == 0
+    # deterministic, and a flipped quotient-root byte or opened value fails
+    # (test_gpu_fullsize.py::test_full_size_wide_air until round 5, which
+    # generated the same 2^20 x 184 trace a second time on the host)
+    assert gpu_ctx.prove(trace, air, pub) == proof
+    for off in (60 + 8, 92 + 5 * 32 + 3):  # quotient root; an opened trace value at zeta
+        bad = bytearray(proof)
+        bad[off] ^= 1
+        assert not gpu_ctx.verify(bytes(bad), air, pub)
     pf, alpha, zeta = _replay(proof, pub_ints, s.perm)
     assert pf.degree_bits == log_n and pf.width == w
 

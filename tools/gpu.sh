@@ -16,6 +16,8 @@
 #   prof             rocprofv3 kernel trace (+ --stats) of a quick bench
 #   pmc              the PMC passes bench.py's roofline reads (tools/pmc_stamp.sh)
 #   rehearse         ranks 0, 5, 7 of the 2^26 proof over 8 ranks (tools/rank_rehearsal.py)
+#   rehearse-red     the same with the redundant inverse forced (LSP_SHARD_SPLIT_INTT=0): the
+#                    other exchange a calibrated 8-GPU run may choose
 #   py:<script>      python <script> under a 300 s limit (tools/ implied), output to a log
 #   h2d              tools/ubench/h2d: host -> device upload modes for a 128 MiB trace (build it first)
 #   tests900:<files> the listed test files with a 900 s per-test limit (the full-size oracle comparisons)
@@ -72,12 +74,14 @@ for step in "$@"; do
       echo "kernel trace in gpurun_out/prof_$TAG" ;;
     pmc)
       bash tools/pmc_stamp.sh pmc_$TAG || exit 1 ;;
-    rehearse)
-      log=gpurun_out/rehearse_$TAG.jsonl
+    rehearse|rehearse-red)
+      log=gpurun_out/${step}_$TAG.jsonl
+      [ "$step" = rehearse-red ] && export LSP_SHARD_SPLIT_INTT=0
       for r in 0 5 7; do
         timeout -k 10 400 python tools/rank_rehearsal.py --log-n 26 --size 8 --ranks $r --steps 2 >> $log \
-          2>> gpurun_out/rehearse_$TAG.err || fail "$step" gpurun_out/rehearse_$TAG.err
+          2>> gpurun_out/${step}_$TAG.err || fail "$step" gpurun_out/${step}_$TAG.err
       done
+      unset LSP_SHARD_SPLIT_INTT
       python -c "
 import json
 for l in open('$log'):

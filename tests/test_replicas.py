@@ -208,3 +208,27 @@ def test_host_pool_mixed_override_does_not_hang(tmp_path, product_lib):
     outs.sort(key=lambda o: o["rank"])
     assert outs[1]["threads"] == 3
     assert 1 <= outs[0]["threads"] <= 16
+
+
+def test_clock_sampler_without_a_gpu(product_lib):
+    """bench.py's box-speed stamp never fails the bench: with no GPU (or no
+    amdsmi device) the sampler says why and reports None, and start/stop are
+    harmless; the summary of given samples is their mean / min / max"""
+    sys.path.insert(0, ROOT)
+    import bench
+    s = bench.ClockSampler(0, period=0.001)
+    assert s.handle is None and s.status != "ok"
+    assert s.start().stop() is None
+    s.samples = [(2100.0, 2000.0, 900.0), (2300.0, None, 1100.0), (None, None, None)]
+    got = s.summary()
+    assert got["sclk_mhz_mean"] == 2200.0 and got["sclk_mhz_min"] == 2100.0 and got["sclk_mhz_max"] == 2300.0
+    assert got["avg_gfxclk_mhz_mean"] == 2000.0 and got["socket_power_w_mean"] == 1000.0 and got["samples"] == 2
+
+
+def test_host_compress_rate(product_lib):
+    """the host half of the box-speed stamp runs on a host-only context"""
+    sys.path.insert(0, ROOT)
+    import bench
+    from linea_stark_prover_amd.prover import Context, StarkConfig
+    with Context(StarkConfig(), device=-1) as ctx:
+        assert bench.host_compress_rate(ctx, n=64, reps=2) > 0

@@ -19,6 +19,9 @@
 #   rehearse-red     the same with the redundant inverse forced (LSP_SHARD_SPLIT_INTT=0): the
 #                    other exchange a calibrated 8-GPU run may choose
 #   py:<script>      python <script> under a 300 s limit (tools/ implied), output to a log
+#   bench8x1         the driver's N = 8 launcher path with 8 ranks sharing this one GPU
+#                    (torch.distributed.run --nproc-per-node 8 bench.py --gpus 8; sharded legs at
+#                    2^20 / 2^22 over gloo, since 8 ranks of 2^26 do not fit one card)
 #   h2d              tools/ubench/h2d: host -> device upload modes for a 128 MiB trace (build it first)
 #   tests900:<files> the listed test files with a 900 s per-test limit (the full-size oracle comparisons)
 #   pmclds:<lib>     one rocprofv3 --pmc pass of the LDS counters (SQ_INSTS_LDS SQ_WAIT_INST_LDS
@@ -87,6 +90,11 @@ import json
 for l in open('$log'):
     if l.startswith('{'):
         d = json.loads(l); print(d['rank'], round(d['prove_s_median'], 4), d['device_used_gib'], d['proof_wire_bytes'])" ;;
+    bench8x1)
+      timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29561 bench.py --gpus 8 --shard-leg 20,22 --batch-leg 20 --no-cpu-baseline \
+        > gpurun_out/bench8x1_$TAG.json 2> gpurun_out/bench8x1_$TAG.err || fail "$step" gpurun_out/bench8x1_$TAG.err
+      grep '^{' gpurun_out/bench8x1_$TAG.json | cut -c1-400 ;;
     h2d)
       timeout -k 10 120 tools/ubench/h2d 128 9 > gpurun_out/h2d_$TAG.json 2>&1 || fail "$step" gpurun_out/h2d_$TAG.json
       cat gpurun_out/h2d_$TAG.json ;;

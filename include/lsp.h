@@ -514,7 +514,7 @@ int lsp_calibrate_poseidon2(lsp_ctx *ctx, double *mperm_per_s);
  * random field elements (h = 2^log_h): the median of 5 timed inverse NTTs
  * after a warm-up, the probe lsp_comm_selftest calibrates the exchange with
  * (log_h 20, w 8) -- random operands, not zeros, since this chip is
- * power-held on MAD-dense work */
+ * power-held on MAD-dense work.  At most 2^28 elements (LSP_E_ARG beyond) */
 int lsp_calibrate_intt(lsp_ctx *ctx, uint32_t log_h, size_t w, double *gelem_per_s);
 
 /* ------------------------------------------------------------- witness */

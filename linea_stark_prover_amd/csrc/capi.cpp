@@ -1395,7 +1395,8 @@ int lsp_calibrate_poseidon2(lsp_ctx* ctx, double* mperm_per_s) {
 int lsp_calibrate_intt(lsp_ctx* ctx, uint32_t log_h, size_t w, double* gelem_per_s) {
     return guarded(ctx, [&] {
         LSP_REQUIRE(ctx && gelem_per_s, LSP_E_ARG, "null argument");
-        LSP_REQUIRE(log_h >= 1 && log_h <= 26 && w >= 1 && w <= 1024, LSP_E_ARG, "bad inverse-NTT probe shape");
+        LSP_REQUIRE(log_h >= 1 && log_h <= 26 && w >= 1 && w <= 1024 && (w << log_h) <= ((size_t)1 << 28), LSP_E_ARG,
+                    "bad inverse-NTT probe shape (at most 2^28 elements)");
         std::lock_guard<std::mutex> g(ctx->mu);
         need_gpu(ctx);
         *gelem_per_s = calibrate_intt(ctx, log_h, w, 5, nullptr);

@@ -53,3 +53,31 @@ def test_intt_probe_matches_the_proofs_inverse_phase(gpu_ctx, monkeypatch):
           f"proof phase {phase_rate:.3f} G elem/s")
     assert abs(rate_shape / phase_rate - 1) < 0.10, (rate_shape, phase_rate)
     assert abs(rate_attach / phase_rate - 1) < 0.10, (rate_attach, phase_rate)
+
+
+def test_box_speed_stamp(gpu_ctx):
+    """bench.py's box-speed stamp on the GPU: the SMU's engine clock sampled
+    while proofs run (amdsmi gpu_metrics, the device matched by bus id), the
+    full-occupancy permutation probe and the host compression rate"""
+    import os
+    import sys
+    import time
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from linea_stark_prover_amd.air import permutation_air
+    from linea_stark_prover_amd.prover import gen_permutation_trace
+    s = bench.ClockSampler(gpu_ctx.device, period=0.01)
+    assert s.status == "ok", s.status
+    a, d, _ = gpu_ctx.config.seeded()
+    tr = gen_permutation_trace(14, 3, a, d)
+    pub = np.concatenate([a, d])
+    s.start()
+    t = time.time()
+    while time.time() - t < 0.3:
+        gpu_ctx.prove(tr, permutation_air(3), pub)
+    got = s.stop()
+    assert got is not None and got["samples"] >= 5, got
+    assert 500 < got["sclk_mhz_mean"] < 3000 and got["sclk_mhz_min"] <= got["sclk_mhz_max"], got
+    box = bench.box_speed(gpu_ctx, got, s.status, 60.0)
+    assert box["gpu_perm_mperm_per_s"] > 100 and box["host_compress_k_per_s"] > 10
+    assert abs(box["ms_per_step_x_sclk_ghz"] - 60.0 * got["sclk_mhz_mean"] / 1e3) < 1e-9

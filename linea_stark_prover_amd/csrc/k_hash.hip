@@ -14,6 +14,7 @@
 #include "k_common.hpp"
 #include "kernels.hpp"
 #include "poseidon2_f29.hpp"
+#include "poseidon2_row.hpp"
 
 namespace lsp {
 
@@ -117,6 +118,23 @@ __global__ __launch_bounds__(256) void k_merkle_level(const Fr* __restrict__ src
     if (!LSP_BOUNDS(2 * i + 1 < 2 * nout)) return;
     const Fr d = compress_f29<D, LANES>(src[2 * i], src[2 * i + 1], rc, rf, rp, qt);
     if ((threadIdx.x & (LANES - 1)) == 0) dst[i] = d;
+}
+
+// The narrowest levels (nout <= row_max(), default linear layers): one node per
+// wave, the state spread over the lanes (poseidon2_row.hpp) -- the level is one
+// compression's single-wave latency, which the 16-lane row product shortens
+template <uint32_t D>
+__global__ __launch_bounds__(64) void k_merkle_level_row(const Fr* __restrict__ src, Fr* __restrict__ dst,
+                                                         size_t nout, const F29* __restrict__ rc, uint32_t rf,
+                                                         uint32_t rp) {
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ prow::RowLds tab;
+    prow::row_lds_init(&tab);
+    __syncthreads();
+    const size_t i = blockIdx.x;
+    if (i >= nout) return;
+    const Fr d = prow::compress_row<D>(src + 2 * i, src + 2 * i + 1, rc, rf, rp, &tab);
+    if (threadIdx.x == 0) dst[i] = d;
 }
 
 // Top of a tree in one workgroup of 4 * 64 lanes: `len` (<= 128, power of
@@ -327,8 +345,27 @@ hipError_t launch_grind(const Fr pre[3], uint32_t wlane, uint64_t base, uint64_t
     return hipGetLastError();
 }
 
+// levels of at most this many nodes run the row form (k_merkle_level_row);
+// LSP_ROW_MAX=0 keeps the quad form
+static size_t row_max() {
+    static const size_t v = [] {
+        const char* e = std::getenv("LSP_ROW_MAX");
+        return e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)1024;
+    }();
+    return v;
+}
+
 hipError_t launch_merkle_level(const Fr* src, Fr* dst, size_t nout, const F29* rc, P2Layout L, hipStream_t st) {
     if (!nout) return hipSuccess;
+    if (!L.gen_lin && nout <= row_max()) {
+        if (L.sbox_degree == 17)
+            hipLaunchKernelGGL(k_merkle_level_row<17>, dim3((unsigned)nout), dim3(64), 0, st, src, dst, nout, rc,
+                               L.rounds_f, L.rounds_p);
+        else
+            hipLaunchKernelGGL(k_merkle_level_row<11>, dim3((unsigned)nout), dim3(64), 0, st, src, dst, nout, rc,
+                               L.rounds_f, L.rounds_p);
+        return hipGetLastError();
+    }
     const int lanes = lanes_for(nout);
     unsigned blocks, bs;
     state_grid(nout, lanes, blocks, bs);

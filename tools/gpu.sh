@@ -18,6 +18,7 @@
 #   rehearse         ranks 0, 5, 7 of the 2^26 proof over 8 ranks (tools/rank_rehearsal.py)
 #   rehearse-red     the same with the redundant inverse forced (LSP_SHARD_SPLIT_INTT=0): the
 #                    other exchange a calibrated 8-GPU run may choose
+#   ub:<name>        the microbenchmark tools/ubench/<name> (built beforehand) under a 120 s limit
 #   py:<script>      python <script> under a 300 s limit (tools/ implied), output to a log
 #   bench8x1         the driver's N = 8 launcher path with 8 ranks sharing this one GPU
 #                    (torch.distributed.run --nproc-per-node 8 bench.py --gpus 8; sharded legs at
@@ -116,6 +117,10 @@ for l in open('$log'):
       LSP_LIB=$PWD/_ab/$lib.so LSP_LIB_OLDER=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d $d -o run -- python3 tools/time_prove.py 19 > $d.log 2>&1 || fail "$step" $d.log
       python tools/prof_summary.py $d/run_kernel_stats.csv 4 > $d.txt 2>&1; head -25 $d.txt ;;
+    ub:*)
+      name=${step#ub:}
+      timeout -k 10 120 tools/ubench/$name > gpurun_out/ub_${name}_$TAG.txt 2>&1 || fail "$step" gpurun_out/ub_${name}_$TAG.txt
+      cat gpurun_out/ub_${name}_$TAG.txt ;;
     py:*)
       script=${step#py:}
       log=gpurun_out/$(basename ${script%% *} .py)_$TAG.log

@@ -169,6 +169,29 @@ def test_merkle_commit_open_verify(gpu_ctx, oracle_lib, logh, widths):
             assert not mmcs.verify_batch(root, widths, logh, idx, rows, bad)
 
 
+# every level on the GPU (LSP_HOST_TREE_TOP=0, read per commit): the row-form
+# compression (k_merkle_level_row) makes the levels of 64..1024 nodes, the quads
+# above them, k_merkle_top the last 128 digests -- each layer against the oracle's
+@pytest.mark.parametrize("logh,widths", [(8, [3]), (11, [1]), (12, [2, 3]), (14, [8])])
+def test_merkle_layers_all_on_gpu(gpu_ctx, oracle_lib, monkeypatch, logh, widths):
+    from linea_stark_prover_amd.prover import MerkleTreeMmcs
+    monkeypatch.setenv("LSP_HOST_TREE_TOP", "0")
+    rng = np.random.default_rng(100 + logh)
+    h = 1 << logh
+    mats = [rand_fr(rng, (h, w)) for w in widths]
+    root, tree = MerkleTreeMmcs(gpu_ctx).commit(mats)
+    cat = np.concatenate(mats, axis=1).copy()
+    layers = np.zeros((2 * h - 1, 4), np.uint64)
+    p = oracle_params(oracle_lib)
+    oracle_lib.lib().lo_merkle_commit(ctypes.byref(p), c_ptr(cat), ctypes.c_size_t(h), ctypes.c_size_t(cat.shape[1]),
+                                      c_ptr(layers), 8)
+    assert np.array_equal(root.reshape(4), layers[-1])
+    off = 0
+    for lv in range(logh + 1):
+        assert np.array_equal(tree.layer(lv), layers[off:off + (h >> lv)]), f"layer {lv}"
+        off += h >> lv
+
+
 # ------------------------------------------------------------------- FRI
 @pytest.mark.parametrize("logn", [1, 3, 10, 14])
 def test_fri_fold_matches_pyoracle_and_fold_row(gpu_ctx, logn):

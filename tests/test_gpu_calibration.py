@@ -5,7 +5,8 @@ sharded proofs choose their exchange on that rate.  Round 5 timed the inverse
 on an all-zero buffer; this chip is power-held on MAD-dense work and zero
 operands draw less power, so that probe could overstate the rate.  The probe
 now runs on seeded random field elements, and here it must agree within 10 %
-with the trace-inverse phase of a real sharded proof at the same shape: rank 0
+with the trace-inverse phase of a real sharded proof at the same shape (and
+within 20 % at the wider shape the self-test probes): rank 0
 of a 2-rank proof of the 3x3 AIR at 2^20 rows (loopback transport, so the
 rank runs alone on the GPU) inverts its w/G = 4 columns of 2^20 as one phase
 ("trace inverse NTT", device events).
@@ -52,7 +53,10 @@ def test_intt_probe_matches_the_proofs_inverse_phase(gpu_ctx, monkeypatch):
     print(f"inverse NTT: probe {rate_shape:.3f} (2^20 x 4), {rate_attach:.3f} (2^20 x 8), "
           f"proof phase {phase_rate:.3f} G elem/s")
     assert abs(rate_shape / phase_rate - 1) < 0.10, (rate_shape, phase_rate)
-    assert abs(rate_attach / phase_rate - 1) < 0.10, (rate_attach, phase_rate)
+    # the probe lsp_comm_selftest runs is 8 columns wide, the phase 4: a wider
+    # matrix inverts faster per element (+3 .. +12 % on the boxes seen), so the
+    # attach-shape figure gets a looser bound than the same-shape one
+    assert abs(rate_attach / phase_rate - 1) < 0.20, (rate_attach, phase_rate)
 
 
 def test_box_speed_stamp(gpu_ctx):

@@ -317,6 +317,7 @@ int lsp_ctx_destroy(lsp_ctx* ctx) {
     }
     if (ctx->ev_near) (void)hipEventDestroy(ctx->ev_near);
     if (ctx->ev_top) (void)hipEventDestroy(ctx->ev_top);
+    if (ctx->ev_warm) (void)hipEventDestroy(ctx->ev_warm);
     if (ctx->side_stream) {
         (void)hipStreamSynchronize(ctx->side_stream);
         (void)hipEventDestroy(ctx->ev_wide);

@@ -102,10 +102,15 @@ void HostPool::loop() {
     for (;;) {
         // spin for a new generation, then sleep
         const auto t0 = std::chrono::steady_clock::now();
+        const int64_t until = std::max<int64_t>(
+            std::chrono::duration_cast<std::chrono::nanoseconds>((t0 + std::chrono::microseconds(kSpinUs)).time_since_epoch())
+                .count(),
+            spin_until_ns_.load(std::memory_order_relaxed));
         for (unsigned it = 0; gen_.load() == seen && !stop_.load(); ++it) {
             cpu_relax();
             if ((it & 255) == 255 &&
-                std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(kSpinUs)) {
+                std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+                        .count() > until) {
                 std::unique_lock<std::mutex> lk(m_);
                 sleepers_.fetch_add(1);  // seq_cst: pairs with parallel_for's gen_ / sleepers_ order
                 cv_.wait(lk, [&] { return stop_.load() || gen_.load() != seen; });
@@ -122,8 +127,13 @@ void HostPool::loop() {
     }
 }
 
-void HostPool::wake() {
+void HostPool::wake(unsigned spin_us) {
     if (th_.empty()) return;
+    if (spin_us)
+        spin_until_ns_.store(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                 (std::chrono::steady_clock::now() + std::chrono::microseconds(spin_us)).time_since_epoch())
+                                 .count(),
+                             std::memory_order_relaxed);
     while (busy_.load() != 0) cpu_relax();
     job_ = nullptr;
     n_ = 0;

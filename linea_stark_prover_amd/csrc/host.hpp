@@ -258,8 +258,10 @@ class HostPool {
     void parallel_for(size_t n, const std::function<void(size_t)>& f);
     // get the workers spinning (they spin kSpinUs for the next job) ahead of a
     // parallel_for whose data is about to arrive: no condition-variable wake-up
-    // on the critical path
-    void wake();
+    // on the critical path.  spin_us > 0: keep spinning until at least that many
+    // microseconds from now (cores that slept through a long GPU phase run the
+    // next parallel_for slower until they have been busy for a while)
+    void wake(unsigned spin_us = 0);
     unsigned size() const { return (unsigned)th_.size() + 1; }
     static constexpr int kSpinUs = 300;
 
@@ -275,6 +277,7 @@ class HostPool {
     std::atomic<unsigned> sleepers_{0};
     std::atomic<uint64_t> gen_{0};
     std::atomic<bool> stop_{false};
+    std::atomic<int64_t> spin_until_ns_{0};  // steady_clock; wake(spin_us)
 };
 // threads of a context's host pool (the caller included): see host.cpp
 unsigned default_host_threads();
@@ -303,6 +306,7 @@ struct lsp_ctx {
     std::map<std::string, Buf> hpool;  // pinned host staging buffers (hbuf)
     std::map<std::string, hipEvent_t> stage_ev;  // last copy out of each h2d_async staging buffer
     hipEvent_t ev_near = nullptr, ev_top = nullptr;  // tree-top hand-off (prove.cpp commit_device)
+    hipEvent_t ev_warm = nullptr;  // after a tree's wide levels: the host pool starts spinning (commit_device)
     // work beside a tree's narrow levels (prove.cpp, "constraints before alpha"):
     // a low-priority stream, the event after the tree's wide levels it waits
     // for, and the event the main stream waits for before using its results

@@ -727,6 +727,19 @@ static bool zerocopy_top() {
 // SIMD or fewer (per-level rates)
 constexpr size_t WIDE_LEVEL_STOP = (size_t)1 << 16;
 
+// The host pool starts spinning when a tree's GPU levels are down to this many
+// digests (ev_warm), not only for the last two levels (ev_near): after a GPU
+// phase of milliseconds the pool's cores, asleep meanwhile, ran the tree top's
+// first parallel_for 20-75 us slower than cores kept busy, unless they had been
+// spinning for about a millisecond (LSP_TIME_TOPS per tree: 2^16 and 2^18 still
+// left the 4M-leaf trees slow, 2^20 -- 1.5-2.7 ms ahead -- made every tree top
+// as fast as the narrow trees').  Read per call; LSP_TOP_WARM=0: off.
+static size_t top_warm_nodes() {
+    const char* e = std::getenv("LSP_TOP_WARM");
+    return e ? (size_t)std::strtoull(e, nullptr, 10) : ((size_t)1 << 20);
+}
+constexpr unsigned TOP_WARM_SPIN_US = 5000;  // bound on the pool's spin after ev_warm
+
 Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, const FoldSpec* fold,
                  const std::function<void(hipEvent_t)>* side) {
     hipStream_t st = ctx->stream;
@@ -773,21 +786,36 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
             }
             return d2h_fr(ctx, layers + 2 * height - 2);
         }
-        // all but the last two GPU levels; an event; the last two (~120 us) and the download
-        size_t off1 = 0, len1 = height;
-        if (side) {  // the wide levels, the side work's event, then the narrow ones
-            size_t offw = 0, lenw = height;
-            LSP_HIP(launch_merkle_levels(layers, height, std::max(4 * top, WIDE_LEVEL_STOP), ctx->rc29_dev, ctx->p2.L,
-                                         &offw, &lenw, st));
-            LSP_HIP(hipEventRecord(ctx->ev_wide, st));
-            LSP_HIP(launch_merkle_levels(layers + offw, lenw, 4 * top, ctx->rc29_dev, ctx->p2.L, &off1, &len1, st));
-            off1 += offw;
-        } else {
-            LSP_HIP(launch_merkle_levels(layers, height, 4 * top, ctx->rc29_dev, ctx->p2.L, &off1, &len1, st));
-        }
         if (!ctx->ev_near) {
             LSP_HIP(hipEventCreateWithFlags(&ctx->ev_near, hipEventDisableTiming));
             LSP_HIP(hipEventCreateWithFlags(&ctx->ev_top, hipEventDisableTiming));
+            LSP_HIP(hipEventCreateWithFlags(&ctx->ev_warm, hipEventDisableTiming));
+        }
+        // the wide levels; the side work's / the host pool's event; the narrow ones
+        // down to 4 top; an event; the last two (~100 us) and the download
+        const size_t warm = top_warm_nodes();
+        // stops (largest first) after which an event goes on the stream
+        struct Stop {
+            size_t nodes;
+            hipEvent_t ev;
+        } stops[2];
+        int nstops = 0;
+        if (warm) stops[nstops++] = {std::max(4 * top, warm), ctx->ev_warm};
+        if (side) stops[nstops++] = {std::max(4 * top, WIDE_LEVEL_STOP), ctx->ev_wide};
+        if (nstops == 2 && stops[1].nodes > stops[0].nodes) std::swap(stops[0], stops[1]);
+        size_t off1 = 0, len1 = height;
+        for (int k = 0; k < nstops; ++k) {
+            size_t o = 0, l = len1;
+            LSP_HIP(launch_merkle_levels(layers + off1, len1, stops[k].nodes, ctx->rc29_dev, ctx->p2.L, &o, &l, st));
+            LSP_HIP(hipEventRecord(stops[k].ev, st));
+            off1 += o;
+            len1 = l;
+        }
+        {
+            size_t o = 0, l = len1;
+            LSP_HIP(launch_merkle_levels(layers + off1, len1, 4 * top, ctx->rc29_dev, ctx->p2.L, &o, &l, st));
+            off1 += o;
+            len1 = l;
         }
         LSP_HIP(hipEventRecord(ctx->ev_near, st));
         size_t off2 = 0, len2 = len1;
@@ -821,10 +849,22 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
         t_launched = clk::now();
         // sleep through the wide levels, then spin (with the pool awake) for the last ones
         resolve_timings(ctx);  // the previous proof's phase events, meanwhile
-        LSP_HIP(hipEventSynchronize(ctx->ev_near));
-        t_near = clk::now();
-        pool.wake();
         hipError_t q;
+        if (warm) {
+            LSP_HIP(hipEventSynchronize(ctx->ev_warm));
+            pool.wake(TOP_WARM_SPIN_US);
+            while ((q = hipEventQuery(ctx->ev_near)) == hipErrorNotReady) {
+#if defined(__x86_64__)
+                __builtin_ia32_pause();
+#endif
+            }
+            LSP_HIP(q);
+            t_near = clk::now();
+        } else {
+            LSP_HIP(hipEventSynchronize(ctx->ev_near));
+            t_near = clk::now();
+            pool.wake();
+        }
         while ((q = hipEventQuery(ctx->ev_top)) == hipErrorNotReady) {
 #if defined(__x86_64__)
             __builtin_ia32_pause();

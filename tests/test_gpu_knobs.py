@@ -3,7 +3,8 @@ bytes unchanged.
 
 The knobs only move work between schedules that compute the same values:
 Merkle levels on the host or the GPU (LSP_HOST_TREE_TOP), FRI rounds on the
-host (LSP_FRI_HOST_TAIL), row / quad / pair / one-lane permutations for narrow
+host (LSP_FRI_HOST_TAIL), when the host pool starts spinning for a tree top
+(LSP_TOP_WARM), row / quad / pair / one-lane permutations for narrow
 levels (LSP_ROW_MAX, LSP_COOP_MAX, LSP_PAIR_MAX), zero-copy tree tops, host subtree tasks, LDE pass
 plans (LSP_NTT_KMAX, LSP_NTT_LOGCW, LSP_NTT_TWL), the host pool size and the
 IFMA host batches.  Several are read once per process, so each setting runs in a
@@ -55,6 +56,8 @@ SETTINGS = {
     "one_lane_levels": {"LSP_COOP_MAX": "0", "LSP_PAIR_MAX": "0", "LSP_ROW_MAX": "0"},
     "quads_to_32k": {"LSP_COOP_MAX": "32768", "LSP_COOP_BS": "256", "LSP_ROW_MAX": "0"},
     "rows_to_16k": {"LSP_ROW_MAX": "16384"},
+    "no_top_warm": {"LSP_TOP_WARM": "0"},
+    "top_warm_64k": {"LSP_TOP_WARM": "65536"},
     "lde_plans": {"LSP_NTT_KMAX": "7", "LSP_NTT_LOGCW": "3", "LSP_NTT_TWL": "0"},
     "host_serial_scalar": {"LSP_HOST_THREADS": "1", "LSP_HOST_IFMA": "0"},
 }

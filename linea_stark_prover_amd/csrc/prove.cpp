@@ -733,10 +733,19 @@ constexpr size_t WIDE_LEVEL_STOP = (size_t)1 << 16;
 // first parallel_for 20-75 us slower than cores kept busy, unless they had been
 // spinning for about a millisecond (LSP_TIME_TOPS per tree: 2^16 and 2^18 still
 // left the 4M-leaf trees slow, 2^20 -- 1.5-2.7 ms ahead -- made every tree top
-// as fast as the narrow trees').  Read per call; LSP_TOP_WARM=0: off.
-static size_t top_warm_nodes() {
-    const char* e = std::getenv("LSP_TOP_WARM");
-    return e ? (size_t)std::strtoull(e, nullptr, 10) : ((size_t)1 << 20);
+// as fast as the narrow trees').  Read per call; LSP_TOP_WARM=0: off.  By
+// default only while this proof has the host to itself: with several proofs in
+// flight in the process or several ranks on the host (LOCAL_WORLD_SIZE > 1) the
+// pools' spinning competed with the other proofs' host work (eight ranks
+// sharing one GPU and 16 CPUs: 19 % slower), for nothing the GPU waits on.
+static size_t top_warm_nodes(const lsp_ctx* ctx) {
+    if (const char* e = std::getenv("LSP_TOP_WARM")) return (size_t)std::strtoull(e, nullptr, 10);
+    static const bool shared_host = [] {
+        const char* e = std::getenv("LOCAL_WORLD_SIZE");
+        return e && std::strtol(e, nullptr, 10) > 1;
+    }();
+    if (shared_host || ctx->comm || g_active_proofs.load(std::memory_order_relaxed) > 1) return 0;
+    return (size_t)1 << 20;
 }
 constexpr unsigned TOP_WARM_SPIN_US = 5000;  // bound on the pool's spin after ev_warm
 
@@ -793,7 +802,7 @@ Fr commit_device(lsp_ctx* ctx, const MatList& m, size_t height, Fr* layers, cons
         }
         // the wide levels; the side work's / the host pool's event; the narrow ones
         // down to 4 top; an event; the last two (~100 us) and the download
-        const size_t warm = top_warm_nodes();
+        const size_t warm = top_warm_nodes(ctx);
         // stops (largest first) after which an event goes on the stream
         struct Stop {
             size_t nodes;
